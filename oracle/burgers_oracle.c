@@ -1,0 +1,303 @@
+/*
+ * burgers_oracle.c -- CPU restatement of the reference FOM hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker: it may be
+ * loaded only by tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg.  The product path (finitedifference_amd) never links,
+ * imports or calls it and fails loudly if its HIP library is missing.
+ *
+ * Parity pinning: the restatement is checked against golden vectors made by
+ * importing the Python reference in the build container
+ * (tests/golden/make_golden.py) and against the author's pickled HDM slices
+ * and SLURM Newton logs (tests/test_oracle_golden.py).
+ *
+ * Reference being restated (paths relative to /root/reference,
+ * C/ = BurgersFD_CleanCoarse/):
+ *   residual        C/hypernet2D.py:2512-2570  inviscid_burgers_res2D_alt
+ *   Jacobian        C/hypernet2D.py:2627-2656  inviscid_burgers_exact_jac2D
+ *   operators       C/hypernet2D.py:2410-2416  make_ddx (backward difference,
+ *                   spdiags([-1/dx, 1/dx], [-1, 0])), :98-106 JDxec/JDyec
+ *   Newton          C/hypernet2D.py:1811-1857  newton_raphson
+ *   linear solve    C/hypernet2D.py:1854       scipy.sparse.linalg.spsolve
+ *                   (SuperLU; third-party).  Restated as the exact 2x2-block
+ *                   forward substitution: in cell-interleaved order the
+ *                   Jacobian is block lower-triangular,
+ *                   so LU of it has no fill and equals this sweep.
+ *   time loop       C/hypernet2D.py:72-131     inviscid_burgers_implicit2D
+ *
+ * Layout (reference): w = [u.ravel(), v.ravel()], u row-major (ny, nx),
+ * cell (r, c) at r*nx + c, v block offset n = nx*ny (C/run_fom.py:33-35).
+ *
+ * Host-side coefficient vectors are computed in Python exactly as NumPy does
+ * in the reference and passed in:
+ *   inv_dx[c] = 1/dx_c,  inv_dy[r] = 1/dy_r         (make_ddx, :2414)
+ *   src[c]    = dt*0.02*exp(mu2*xc_c)               (:2550)
+ *   lbc[r]    = 0.5*dt*mu1**2/dx[r]  (row-indexed quirk of :2553-2554)
+ *
+ * The closed-form march (orc_march_step) is NOT a reference function: it is
+ * the build's own exact solver for the same implicit step
+ * and is restated here op-for-op as the bitwise checker of the HIP march.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define IDX(r, c, nx) ((size_t)(r) * (size_t)(nx) + (size_t)(c))
+
+/* ------------------------------------------------------------------------ */
+/* Residual: mirror of inviscid_burgers_res2D_alt (C/hypernet2D.py:2512-2570),
+ * keeping NumPy's operation order:
+ *   ru = u - up + (a*JDx)@(Fu+Fpu) + (a*JDy)@(Fuv+Fpuv) - src ; ru -= lbc
+ *   rv = v - vp + (a*JDy)@(Fv+Fpv) + a*(JDx@(Fuv+Fpuv))
+ * with a = 0.5*dt.  A sparse row holds two entries, so the matvec sum is
+ * order-independent: (D f)_i = k_i f_i - k_{i-1} f_{i-1}.                    */
+void orc_residual(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                  const double *src, const double *lbc, double dt,
+                  const double *w, const double *wp, double *res)
+{
+    const size_t n = (size_t)nx * ny;
+    const double a = 0.5 * dt;
+    const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
+    for (int r = 0; r < ny; ++r) {
+        const double ay = a * inv_dy[r];
+        const double ays = r > 0 ? a * inv_dy[r - 1] : 0.0;
+        for (int c = 0; c < nx; ++c) {
+            const size_t i = IDX(r, c, nx);
+            const double ax = a * inv_dx[c];
+            /* fluxes at this cell */
+            const double Su = 0.5 * (u[i] * u[i]) + 0.5 * (up[i] * up[i]);
+            const double Sv = 0.5 * (v[i] * v[i]) + 0.5 * (vp[i] * vp[i]);
+            const double Suv = (0.5 * u[i]) * v[i] + (0.5 * up[i]) * vp[i];
+            double dxu = ax * Su, dyuv = ay * Suv, dyv = ay * Sv, dxuv = inv_dx[c] * Suv;
+            if (c > 0) {
+                const size_t j = i - 1;
+                const double axw = a * inv_dx[c - 1];
+                const double SuW = 0.5 * (u[j] * u[j]) + 0.5 * (up[j] * up[j]);
+                const double SuvW = (0.5 * u[j]) * v[j] + (0.5 * up[j]) * vp[j];
+                dxu = dxu + (-axw) * SuW;
+                dxuv = dxuv + (-inv_dx[c - 1]) * SuvW;
+            }
+            if (r > 0) {
+                const size_t j = i - (size_t)nx;
+                const double SvS = 0.5 * (v[j] * v[j]) + 0.5 * (vp[j] * vp[j]);
+                const double SuvS = (0.5 * u[j]) * v[j] + (0.5 * up[j]) * vp[j];
+                dyuv = dyuv + (-ays) * SuvS;
+                dyv = dyv + (-ays) * SvS;
+            }
+            double ru = u[i] - up[i];
+            ru = ru + dxu;
+            ru = ru + dyuv;
+            ru = ru - src[c];
+            ru = ru - (c == 0 ? lbc[r] : 0.0);
+            double rv = v[i] - vp[i];
+            rv = rv + dyv;
+            rv = rv + a * dxuv;
+            res[i] = ru;
+            res[n + i] = rv;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Jacobian-vector product: J(w) x with J from inviscid_burgers_exact_jac2D
+ * (C/hypernet2D.py:2627-2656):
+ *   J = I + [[JDx D(au) + 0.5 JDy D(av), 0.5 JDy D(au)],
+ *            [0.5 JDx D(av),            JDy D(av) + 0.5 JDx D(au)]]
+ * Matrix-free, per cell with the linearised fluxes
+ *   XFd = ax u xu,  XHd = 0.5 ax (v xu + u xv),
+ *   YHd = 0.5 ay (v xu + u xv),  YGd = ay v xv,
+ *   (Jx)_u = xu + XFd - XFd_W + YHd - YHd_S,
+ *   (Jx)_v = xv + YGd - YGd_S + XHd - XHd_W.                                  */
+void orc_jvp(int nx, int ny, const double *inv_dx, const double *inv_dy, double dt,
+             const double *w, const double *x, double *y)
+{
+    const size_t n = (size_t)nx * ny;
+    const double a = 0.5 * dt;
+    const double *u = w, *v = w + n, *xu = x, *xv = x + n;
+    for (int r = 0; r < ny; ++r) {
+        for (int c = 0; c < nx; ++c) {
+            const size_t i = IDX(r, c, nx);
+            const double ax = a * inv_dx[c], ay = a * inv_dy[r];
+            const double m = v[i] * xu[i] + u[i] * xv[i];
+            double yu = xu[i] + ax * u[i] * xu[i] + 0.5 * ay * m;
+            double yv = xv[i] + ay * v[i] * xv[i] + 0.5 * ax * m;
+            if (c > 0) {
+                const size_t j = i - 1;
+                const double axw = a * inv_dx[c - 1];
+                const double mW = v[j] * xu[j] + u[j] * xv[j];
+                yu -= axw * u[j] * xu[j];
+                yv -= 0.5 * axw * mW;
+            }
+            if (r > 0) {
+                const size_t j = i - (size_t)nx;
+                const double ays = a * inv_dy[r - 1];
+                const double mS = v[j] * xu[j] + u[j] * xv[j];
+                yu -= 0.5 * ays * mS;
+                yv -= ays * v[j] * xv[j];
+            }
+            y[i] = yu;
+            y[n + i] = yv;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* Exact solve J(w) delta = rhs: 2x2-block forward substitution in
+ * lexicographic (r, c) order.  Replaces spsolve (C/hypernet2D.py:1854); the
+ * Jacobian is block lower-triangular in cell order, so this is the LU solve
+ * with zero fill.                                                            */
+void orc_block_solve(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                     double dt, const double *w, const double *rhs, double *delta)
+{
+    const size_t n = (size_t)nx * ny;
+    const double a = 0.5 * dt;
+    const double *u = w, *v = w + n;
+    double *du = delta, *dv = delta + n;
+    for (int r = 0; r < ny; ++r) {
+        for (int c = 0; c < nx; ++c) {
+            const size_t i = IDX(r, c, nx);
+            const double ax = a * inv_dx[c], ay = a * inv_dy[r];
+            double eu = rhs[i], ev = rhs[n + i];
+            if (c > 0) {
+                const size_t j = i - 1;
+                const double axw = a * inv_dx[c - 1];
+                eu += axw * u[j] * du[j];
+                ev += 0.5 * axw * (v[j] * du[j] + u[j] * dv[j]);
+            }
+            if (r > 0) {
+                const size_t j = i - (size_t)nx;
+                const double ays = a * inv_dy[r - 1];
+                eu += 0.5 * ays * (v[j] * du[j] + u[j] * dv[j]);
+                ev += ays * v[j] * dv[j];
+            }
+            const double a00 = 1.0 + ax * u[i] + 0.5 * ay * v[i];
+            const double a01 = 0.5 * ay * u[i];
+            const double a10 = 0.5 * ax * v[i];
+            const double a11 = 1.0 + ay * v[i] + 0.5 * ax * u[i];
+            const double det = a00 * a11 - a01 * a10;
+            du[i] = (a11 * eu - a01 * ev) / det;
+            dv[i] = (a00 * ev - a10 * eu) / det;
+        }
+    }
+}
+
+static double norm2(const double *x, size_t m)
+{
+    double s = 0.0;
+    for (size_t i = 0; i < m; ++i) s += x[i] * x[i];
+    return sqrt(s);
+}
+
+/* ------------------------------------------------------------------------ */
+/* One implicit step by newton_raphson (C/hypernet2D.py:1811-1857):
+ *   x = x0; init = ||R(x0)||; for i < max_its: rn = ||R(x)||;
+ *   if rn/init < cutoff: break; x -= J(x)^{-1} R(x).
+ * Returns the number of updates taken (the printed "i"); *final_rel gets the
+ * last rn/init.  w_out may alias nothing; scratch is allocated here.         */
+int orc_newton_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                    const double *src, const double *lbc, double dt,
+                    const double *wp, double *w_out, int max_its, double cutoff,
+                    double *final_rel)
+{
+    const size_t m = 2 * (size_t)nx * ny;
+    double *res = (double *)malloc(m * sizeof(double));
+    double *del = (double *)malloc(m * sizeof(double));
+    memcpy(w_out, wp, m * sizeof(double));
+    orc_residual(nx, ny, inv_dx, inv_dy, src, lbc, dt, wp, wp, res);
+    const double init = norm2(res, m);
+    int it = 0;
+    double rel = NAN;
+    for (it = 0; it < max_its; ++it) {
+        orc_residual(nx, ny, inv_dx, inv_dy, src, lbc, dt, w_out, wp, res);
+        rel = norm2(res, m) / init;
+        if (rel < cutoff) break;
+        orc_block_solve(nx, ny, inv_dx, inv_dy, dt, w_out, res, del);
+        for (size_t i = 0; i < m; ++i) w_out[i] -= del[i];
+    }
+    if (final_rel) *final_rel = rel;
+    free(res);
+    free(del);
+    return it;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Closed-form march (build's own exact solver; DESIGN.md section 3 "MARCH SPEC").
+ * The implicit residual is lower-triangular in (r, c) and each cell's 2x2
+ * system is u*s = Cu, v*s = Cv with the common factor s = 1 + hx u + hy v,
+ * so s = 0.5 + sqrt(0.25 + hx Cu + hy Cv).  Op order is normative: the HIP
+ * march reproduces it bit for bit.                                            */
+void orc_march_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                    const double *src, const double *lbc, double dt,
+                    const double *wp, double *w)
+{
+    const size_t n = (size_t)nx * ny;
+    const double a = 0.5 * dt;
+    const double *up = wp, *vp = wp + n;
+    double *u = w, *v = w + n;
+    /* outflows of the row below (YH, YG) and of the west cell (XF, XH) */
+    double *yh = (double *)calloc((size_t)nx, sizeof(double));
+    double *yg = (double *)calloc((size_t)nx, sizeof(double));
+    for (int r = 0; r < ny; ++r) {
+        const double ay = a * inv_dy[r];
+        const double hy = 0.5 * ay;
+        double xfw = 0.0, xhw = 0.0;
+        for (int c = 0; c < nx; ++c) {
+            const size_t i = IDX(r, c, nx);
+            const double ax = a * inv_dx[c];
+            const double hx = 0.5 * ax;
+            const double sl = c == 0 ? src[0] + lbc[r] : src[c];
+            const double pu = up[i], pv = vp[i];
+            const double hu = 0.5 * pu;
+            const double xfp = ax * (hu * pu);
+            const double xhp = ax * (hu * pv);
+            const double yhp = ay * (hu * pv);
+            const double ygp = ay * ((0.5 * pv) * pv);
+            const double bu = ((pu - xfp) - yhp) + sl;
+            const double bv = (pv - ygp) - xhp;
+            const double cu = (bu + xfw) + yh[c];
+            const double cv = (bv + yg[c]) + xhw;
+            const double mm = fma(hx, cu, hy * cv);
+            const double s = 0.5 + sqrt(0.25 + mm);
+            const double rs = 1.0 / s;
+            const double nu = cu * rs, nv = cv * rs;
+            const double hxu = hx * nu;
+            xfw = fma(hxu, nu, xfp);
+            xhw = fma(hxu, nv, xhp);
+            yh[c] = fma(hy * nu, nv, yhp);
+            yg[c] = fma(hy * nv, nv, ygp);
+            u[i] = nu;
+            v[i] = nv;
+        }
+    }
+    free(yh);
+    free(yg);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Time loop (C/hypernet2D.py:72-131).  snaps is step-major:
+ * (num_steps+1) x 2n, row j = state after j steps.  solver 0 = newton (the
+ * reference algorithm), 1 = closed-form march.  newton_its[i] (may be NULL)
+ * receives the Newton update count of step i.                                */
+int orc_fom(int nx, int ny, const double *inv_dx, const double *inv_dy,
+            const double *src, const double *lbc, double dt, const double *w0,
+            int num_steps, int solver, int max_its, double cutoff,
+            double *snaps, int *newton_its, double *final_rel)
+{
+    const size_t m = 2 * (size_t)nx * ny;
+    memcpy(snaps, w0, m * sizeof(double));
+    for (int i = 0; i < num_steps; ++i) {
+        const double *wp = snaps + (size_t)i * m;
+        double *w = snaps + (size_t)(i + 1) * m;
+        if (solver == 0) {
+            double rel = 0.0;
+            int its = orc_newton_step(nx, ny, inv_dx, inv_dy, src, lbc, dt, wp, w,
+                                      max_its, cutoff, &rel);
+            if (newton_its) newton_its[i] = its;
+            if (final_rel) final_rel[i] = rel;
+        } else {
+            orc_march_step(nx, ny, inv_dx, inv_dy, src, lbc, dt, wp, w);
+        }
+    }
+    return 0;
+}
