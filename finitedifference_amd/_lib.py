@@ -1,0 +1,135 @@
+"""ctypes binding of libburgers_hip.so (C ABI: include/burgers.h).
+
+The product path has exactly one compute backend: the HIP library built for
+gfx950 (finitedifference_amd/csrc, ``python -m finitedifference_amd.build`` or
+``__graft_entry__.build()``).  There is no CPU fallback: if the library is
+missing, or no MI355X is visible, every compute call raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
+ABI_VERSION = 1
+
+BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_ERCCL = 0, -1, -2, -3, -4
+BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
+SOLVERS = {"march": 0, "newton": 1}
+
+# Every symbol include/burgers.h declares (checked by tests/test_capi.py).
+EXPORTS = (
+    "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_rccl_unique_id",
+    "burg_ctx_create_slab", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
+    "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
+    "burg_advance", "burg_download_state",
+)
+
+
+class BurgStats(ctypes.Structure):
+    """Mirror of struct burg_stats (include/burgers.h)."""
+    _fields_ = [
+        ("steps", ctypes.c_int64),
+        ("tile_marches", ctypes.c_int64),
+        ("passes", ctypes.c_int64),
+        ("max_passes", ctypes.c_int32),
+        ("unconverged_steps", ctypes.c_int32),
+        ("newton_updates", ctypes.c_int64),
+        ("newton_max_updates", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
+        ("loop_ms", ctypes.c_double),
+        ("flush_ms", ctypes.c_double),
+        ("march_kernel_ms", ctypes.c_double),
+        ("march_launches", ctypes.c_int64),
+        ("last_rel", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class BurgersError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"libburgers_hip error {code}: {msg}")
+        self.code = code
+
+
+class NotConvergedWarning(UserWarning):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+_D = ctypes.POINTER(ctypes.c_double)
+_I32 = ctypes.POINTER(ctypes.c_int32)
+_VP = ctypes.c_void_p
+
+
+def load(path=None):
+    """Load (once) and return the HIP library; raises if it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise RuntimeError(
+                f"{p} is missing: build the HIP extension first "
+                "(python -c 'import __graft_entry__ as g; g.build()' or make -C "
+                "finitedifference_amd/csrc). There is no CPU fallback.")
+        lib = ctypes.CDLL(p)
+        sig = {
+            "burg_abi_version": (ctypes.c_int, []),
+            "burg_last_error": (ctypes.c_char_p, []),
+            "burg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.POINTER(_VP)]),
+            "burg_rccl_unique_id": (ctypes.c_int, [_VP]),
+            "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [_VP, ctypes.POINTER(_VP)]),
+            "burg_ctx_destroy": (None, [_VP]),
+            "burg_set_problem": (ctypes.c_int, [_VP, _D, _D, _D, _D, ctypes.c_double]),
+            "burg_set_options": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
+                                                ctypes.c_double, ctypes.c_int]),
+            "burg_residual": (ctypes.c_int, [_VP, _D, _D, _D, _D]),
+            "burg_jvp": (ctypes.c_int, [_VP, _D, _D, _D]),
+            "burg_block_solve": (ctypes.c_int, [_VP, _D, _D, _D]),
+            "burg_run": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                        ctypes.c_double, _D, ctypes.c_int64, ctypes.c_int,
+                                        ctypes.POINTER(BurgStats), _I32, _D]),
+            "burg_upload_state": (ctypes.c_int, [_VP, _D]),
+            "burg_advance": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
+                                            ctypes.POINTER(BurgStats)]),
+            "burg_download_state": (ctypes.c_int, [_VP, _D]),
+        }
+        for name, (res, args) in sig.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.burg_abi_version()
+        if v != ABI_VERSION:
+            raise RuntimeError(f"{p}: ABI version {v}, expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def check(code, allow=()):
+    if code == BURG_OK or code in allow:
+        return code
+    msg = load().burg_last_error().decode(errors="replace")
+    raise BurgersError(code, msg)
+
+
+def dptr(a):
+    """double* of a C-contiguous float64 array (None -> NULL)."""
+    if a is None:
+        return None
+    assert a.dtype == np.float64 and a.flags.c_contiguous, "need C-contiguous float64"
+    return a.ctypes.data_as(_D)
+
+
+def iptr(a):
+    if a is None:
+        return None
+    assert a.dtype == np.int32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_I32)

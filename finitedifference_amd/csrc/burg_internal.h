@@ -1,0 +1,79 @@
+// burg_internal.h -- shared device/host declarations of libburgers_hip.so.
+//
+// Layout in HBM: every field is a row-major (ny, nx) fp64
+// plane; a state is [u plane | v plane] exactly as the reference's
+// w = [u.ravel(), v.ravel()] (C/run_fom.py:33-35), so device state <-> host
+// snapshot column copies are plain memcpy/transposes.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace burg {
+
+constexpr int kWave = 64;  // CDNA wavefront; also the tile height (one lane per row)
+
+// Per-problem coefficient vectors (device pointers, slab-local rows).
+struct Coeffs {
+    const double *inv_dx;  // [nx]      1/dx_c
+    const double *inv_dy;  // [ny]      1/dy_r   (rows of this slab)
+    const double *src;     // [nx]      dt*0.02*exp(mu2*xc)
+    const double *lbc;     // [ny]      0.5*dt*mu1^2/dx[r] (inlet, column 0 only)
+    double alpha;          // 0.5*dt
+    int nx, ny;            // local grid (ny = rows owned by this slab)
+};
+
+// Tile engine bookkeeping.  A tile is 64 rows x tw columns,
+// marched by one wavefront.  Edge planes hold, per tile, the two outflow
+// quantities of its east column (E: 2 x 64) and north row (N: 2 x tw); two
+// generations (ping-pong by pass parity).  Wused/Sused keep the inflow each
+// tile was last marched with.
+struct Engine {
+    double *eb[2];     // [ntiles][2][64]
+    double *nb[2];     // [ntiles][2][tw]
+    double *wused;     // [ntiles][2][64]
+    double *sused;     // [ntiles][2][tw]
+    int *counters;     // [kmax + 2]  tiles marched per pass (index = pass)
+    // Slab halo (multi-GPU): outflow (YH, YG) of the row below this slab,
+    // [2][nx], and that row's previous-step state (u, v) [2][nx] for the
+    // pass-1 guess.  nullptr => bottom rows see the domain boundary (zero).
+    const double *halo_flux;
+    const double *halo_wp;
+    double tol;        // relative inflow motion that triggers a re-march
+    int nti, ntj;      // tile grid
+    int tw;            // tile width
+};
+
+// Accumulated per-run statistics kept on the device.
+struct DevStats {
+    long long tile_marches;
+    long long passes;
+    int max_passes;
+    int unconverged_steps;
+    long long steps;
+};
+
+}  // namespace burg
+
+// ---- host-side launch wrappers (defined in the .hip files) ----------------
+namespace burg {
+
+int launch_march_pass(const Coeffs &cf, const Engine &eg, const double *wp, double *w,
+                      int pass, hipStream_t st);
+int launch_solve_pass(const Coeffs &cf, const Engine &eg, const double *w,
+                      const double *rhs, double *delta, int pass, hipStream_t st);
+int launch_pass_epilogue(const Engine &eg, int kmax, DevStats *stats, hipStream_t st);
+
+int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
+                    double *partials, double *sumsq, const double *halo_w,
+                    const double *halo_wp, hipStream_t st);
+int residual_partials_count(const Coeffs &cf);
+int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y,
+               hipStream_t st);
+int launch_axpy_neg(double *w, const double *d, size_t m, hipStream_t st);
+int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
+                     int ldo, hipStream_t st);
+
+}  // namespace burg

@@ -1,0 +1,649 @@
+// capi.hip -- C ABI (include/burgers.h) of libburgers_hip.so: contexts, the
+// time loop (inviscid_burgers_implicit2D, C/hypernet2D.py:72-131) and the
+// parity hooks.  Host-side only; kernels live in march.hip / stencil.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/burgers.h"
+#include "burg_internal.h"
+
+using namespace burg;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char *fmt, ...)
+{
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (expr);                                                         \
+        if (e_ != hipSuccess)                                                           \
+            return fail(BURG_EHIP, "%s:%d %s: %s", __FILE__, __LINE__, #expr,           \
+                        hipGetErrorString(e_));                                         \
+    } while (0)
+
+#define CHK(expr)                                                                       \
+    do {                                                                                \
+        int c_ = (expr);                                                                \
+        if (c_ != 0) {                                                                  \
+            if (c_ == -3)                                                               \
+                return fail(BURG_EHIP, "%s:%d kernel launch %s: %s", __FILE__, __LINE__, \
+                            #expr, hipGetErrorString(hipGetLastError()));               \
+            return c_;                                                                  \
+        }                                                                               \
+    } while (0)
+
+template <class T>
+int dalloc(T **p, size_t count)
+{
+    *p = nullptr;
+    if (count == 0) return 0;
+    hipError_t e = hipMalloc((void **)p, count * sizeof(T));
+    if (e != hipSuccess)
+        return fail(BURG_ENOMEM, "hipMalloc(%zu bytes): %s", count * sizeof(T),
+                    hipGetErrorString(e));
+    return 0;
+}
+
+template <class T>
+void dfree(T *&p)
+{
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+}  // namespace
+
+struct burg_ctx {
+    int device = 0;
+    int nx = 0, ny_total = 0, row0 = 0, nrows = 0;
+    int rank = 0, world = 1;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+    // problem (global arrays on device; cf views this slab's rows)
+    bool have_problem = false;
+    double dt = 0.0;
+    double *d_inv_dx = nullptr, *d_inv_dy = nullptr, *d_src = nullptr, *d_lbc = nullptr;
+    Coeffs cf{};
+
+    // engine
+    int tw = 64, max_passes_opt = 0, profile = 0;
+    double tol = 0x1p-50;  // 4 ulp relative
+    Engine eg{};
+    int kmax = 0;
+    double *d_edges = nullptr;
+    int *d_counters = nullptr;
+    DevStats *d_stats = nullptr;
+
+    // states (ping-pong) and scratch
+    double *d_state[2] = {nullptr, nullptr};
+    int cur = 0;
+    double *d_r = nullptr, *d_d = nullptr, *d_x = nullptr, *d_partials = nullptr,
+           *d_sumsq = nullptr;
+    int npartials = 0;
+    std::vector<hipEvent_t> prof_ev;
+
+    size_t m() const { return 2 * (size_t)nx * nrows; }
+    size_t n() const { return (size_t)nx * nrows; }
+};
+
+namespace {
+
+int engine_alloc(burg_ctx *c)
+{
+    dfree(c->d_edges);
+    dfree(c->d_counters);
+    const int nti = (c->nrows + kWave - 1) / kWave;
+    const int ntj = (c->nx + c->tw - 1) / c->tw;
+    const size_t nt = (size_t)nti * ntj;
+    const size_t per_e = 2 * (size_t)kWave, per_n = 2 * (size_t)c->tw;
+    const size_t total = nt * (2 * per_e + 2 * per_n + per_e + per_n);
+    if (int e = dalloc(&c->d_edges, total)) return e;
+    HIPCHK(hipMemsetAsync(c->d_edges, 0, total * sizeof(double), c->stream));
+    double *p = c->d_edges;
+    c->eg.eb[0] = p;
+    p += nt * per_e;
+    c->eg.eb[1] = p;
+    p += nt * per_e;
+    c->eg.nb[0] = p;
+    p += nt * per_n;
+    c->eg.nb[1] = p;
+    p += nt * per_n;
+    c->eg.wused = p;
+    p += nt * per_e;
+    c->eg.sused = p;
+    c->eg.nti = nti;
+    c->eg.ntj = ntj;
+    c->eg.tw = c->tw;
+    c->eg.tol = c->tol;
+    c->eg.halo_flux = nullptr;
+    c->eg.halo_wp = nullptr;
+    const int bound = nti + ntj;  // #anti-diagonals + 1 passes always reach the fixed point
+    c->kmax = c->max_passes_opt > 0 ? std::min(c->max_passes_opt, bound) : bound;
+    if (int e = dalloc(&c->d_counters, (size_t)c->kmax + 2)) return e;
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, sizeof(int) * (c->kmax + 2), c->stream));
+    c->eg.counters = c->d_counters;
+    return 0;
+}
+
+int ensure_scratch(burg_ctx *c)
+{
+    if (c->d_r) return 0;
+    if (int e = dalloc(&c->d_r, c->m())) return e;
+    if (int e = dalloc(&c->d_d, c->m())) return e;
+    if (int e = dalloc(&c->d_x, c->m())) return e;
+    c->npartials = residual_partials_count(c->cf);
+    if (int e = dalloc(&c->d_partials, (size_t)c->npartials)) return e;
+    if (int e = dalloc(&c->d_sumsq, 1)) return e;
+    return 0;
+}
+
+int check_ready(burg_ctx *c)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (!c->have_problem) return fail(BURG_ESTATE, "burg_set_problem has not been called");
+    HIPCHK(hipSetDevice(c->device));
+    return 0;
+}
+
+// One implicit step wp -> w by the march engine (all passes + epilogue).
+int march_step(burg_ctx *c, const double *wp, double *w)
+{
+    for (int k = 1; k <= c->kmax; ++k) {
+        if (c->profile) {
+            hipEvent_t a, b;
+            HIPCHK(hipEventCreate(&a));
+            HIPCHK(hipEventCreate(&b));
+            HIPCHK(hipEventRecord(a, c->stream));
+            CHK(launch_march_pass(c->cf, c->eg, wp, w, k, c->stream));
+            HIPCHK(hipEventRecord(b, c->stream));
+            c->prof_ev.push_back(a);
+            c->prof_ev.push_back(b);
+        } else {
+            CHK(launch_march_pass(c->cf, c->eg, wp, w, k, c->stream));
+        }
+    }
+    CHK(launch_pass_epilogue(c->eg, c->kmax, c->d_stats, c->stream));
+    return 0;
+}
+
+// Exact linear solve J(w) delta = rhs with the SOLVE cell.
+int block_solve(burg_ctx *c, const double *w, const double *rhs, double *delta)
+{
+    for (int k = 1; k <= c->kmax; ++k)
+        CHK(launch_solve_pass(c->cf, c->eg, w, rhs, delta, k, c->stream));
+    CHK(launch_pass_epilogue(c->eg, c->kmax, c->d_stats, c->stream));
+    return 0;
+}
+
+int residual_norm(burg_ctx *c, const double *w, const double *wp, double *r, double *norm)
+{
+    CHK(launch_residual(c->cf, w, wp, r, c->d_partials, c->d_sumsq, nullptr, nullptr,
+                        c->stream));
+    double s = 0.0;
+    HIPCHK(hipMemcpyAsync(&s, c->d_sumsq, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    *norm = std::sqrt(s);
+    return 0;
+}
+
+// newton_raphson (C/hypernet2D.py:1811-1857) for one step, on the device:
+// x = wp; init = ||R(wp)||; loop: rn = ||R(x)||; stop if rn/init < rtol;
+// x -= J(x)^{-1} R(x).  Returns the number of updates.
+int newton_step(burg_ctx *c, const double *wp, double *w, int max_its, double rtol,
+                int *its_out, double *rel_out)
+{
+    HIPCHK(hipMemcpyAsync(w, wp, c->m() * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    double init = 0.0, rn = 0.0, rel = NAN;
+    if (int e = residual_norm(c, wp, wp, c->d_r, &init)) return e;
+    int it = 0;
+    for (it = 0; it < max_its; ++it) {
+        if (int e = residual_norm(c, w, wp, c->d_r, &rn)) return e;
+        rel = rn / init;
+        if (!std::isfinite(rn)) return fail(BURG_ENAN, "non-finite residual norm in Newton");
+        if (rel < rtol) break;
+        if (int e = block_solve(c, w, c->d_r, c->d_d)) return e;
+        CHK(launch_axpy_neg(w, c->d_d, c->m(), c->stream));
+    }
+    *its_out = it;
+    *rel_out = rel;
+    return 0;
+}
+
+void collect_profile(burg_ctx *c, burg_stats *st)
+{
+    if (c->prof_ev.empty()) return;
+    (void)hipStreamSynchronize(c->stream);
+    double ms = 0.0;
+    for (size_t i = 0; i + 1 < c->prof_ev.size(); i += 2) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, c->prof_ev[i], c->prof_ev[i + 1]);
+        ms += t;
+        (void)hipEventDestroy(c->prof_ev[i]);
+        (void)hipEventDestroy(c->prof_ev[i + 1]);
+    }
+    if (st) {
+        st->march_kernel_ms += ms;
+        st->march_launches += (int64_t)(c->prof_ev.size() / 2);
+    }
+    c->prof_ev.clear();
+}
+
+int read_stats(burg_ctx *c, burg_stats *st)
+{
+    DevStats ds{};
+    HIPCHK(hipMemcpyAsync(&ds, c->d_stats, sizeof ds, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (st) {
+        st->steps = ds.steps;
+        st->tile_marches = ds.tile_marches;
+        st->passes = ds.passes;
+        st->max_passes = ds.max_passes;
+        st->unconverged_steps = ds.unconverged_steps;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int burg_abi_version(void) { return BURG_ABI_VERSION; }
+
+const char *burg_last_error(void) { return g_err.c_str(); }
+
+int burg_ctx_create(int device, int nx, int ny, burg_ctx **out)
+{
+    return burg_ctx_create_slab(device, nx, ny, 0, ny, 0, 1, nullptr, out);
+}
+
+int burg_rccl_unique_id(void *id_out)
+{
+    if (!id_out) return fail(BURG_EINVAL, "null id buffer");
+    return fail(BURG_ERCCL, "multi-GPU slabs are not built into this library yet");
+}
+
+int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, int rank,
+                         int world, const void *nccl_id, burg_ctx **out)
+{
+    if (!out) return fail(BURG_EINVAL, "null out pointer");
+    *out = nullptr;
+    if (nx < 1 || ny_total < 1 || row0 < 0 || nrows < 1 || row0 + nrows > ny_total)
+        return fail(BURG_EINVAL, "bad grid: nx=%d ny=%d row0=%d nrows=%d", nx, ny_total, row0,
+                    nrows);
+    if (world != 1 || rank != 0 || row0 != 0 || nrows != ny_total)
+        return fail(BURG_ERCCL, "multi-GPU slabs are not built into this library yet");
+    (void)nccl_id;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev)
+        return fail(BURG_EINVAL, "device %d out of range (%d visible)", device, ndev);
+    HIPCHK(hipSetDevice(device));
+    burg_ctx *c = new burg_ctx();
+    c->device = device;
+    c->nx = nx;
+    c->ny_total = ny_total;
+    c->row0 = row0;
+    c->nrows = nrows;
+    c->rank = rank;
+    c->world = world;
+    int e = 0;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+        burg_ctx_destroy(c);
+        return fail(BURG_EHIP, "stream/event creation failed");
+    }
+    if ((e = dalloc(&c->d_state[0], c->m())) || (e = dalloc(&c->d_state[1], c->m())) ||
+        (e = dalloc(&c->d_stats, 1))) {
+        burg_ctx_destroy(c);
+        return e;
+    }
+    (void)hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream);
+    if ((e = engine_alloc(c))) {
+        burg_ctx_destroy(c);
+        return e;
+    }
+    *out = c;
+    return BURG_OK;
+}
+
+void burg_ctx_destroy(burg_ctx *c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (auto ev : c->prof_ev) (void)hipEventDestroy(ev);
+    dfree(c->d_inv_dx);
+    dfree(c->d_inv_dy);
+    dfree(c->d_src);
+    dfree(c->d_lbc);
+    dfree(c->d_edges);
+    dfree(c->d_counters);
+    dfree(c->d_stats);
+    dfree(c->d_state[0]);
+    dfree(c->d_state[1]);
+    dfree(c->d_r);
+    dfree(c->d_d);
+    dfree(c->d_x);
+    dfree(c->d_partials);
+    dfree(c->d_sumsq);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int burg_set_problem(burg_ctx *c, const double *inv_dx, const double *inv_dy,
+                     const double *src, const double *lbc, double dt)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (!inv_dx || !inv_dy || !src || !lbc) return fail(BURG_EINVAL, "null coefficient array");
+    if (!(dt > 0.0) || !std::isfinite(dt)) return fail(BURG_EINVAL, "dt must be > 0");
+    HIPCHK(hipSetDevice(c->device));
+    if (!c->d_inv_dx) {
+        if (int e = dalloc(&c->d_inv_dx, (size_t)c->nx)) return e;
+        if (int e = dalloc(&c->d_inv_dy, (size_t)c->ny_total)) return e;
+        if (int e = dalloc(&c->d_src, (size_t)c->nx)) return e;
+        if (int e = dalloc(&c->d_lbc, (size_t)c->ny_total)) return e;
+    }
+    HIPCHK(hipMemcpyAsync(c->d_inv_dx, inv_dx, sizeof(double) * c->nx, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_inv_dy, inv_dy, sizeof(double) * c->ny_total,
+                          hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_src, src, sizeof(double) * c->nx, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_lbc, lbc, sizeof(double) * c->ny_total, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->dt = dt;
+    c->cf.inv_dx = c->d_inv_dx;
+    c->cf.inv_dy = c->d_inv_dy + c->row0;
+    c->cf.src = c->d_src;
+    c->cf.lbc = c->d_lbc + c->row0;
+    c->cf.alpha = 0.5 * dt;
+    c->cf.nx = c->nx;
+    c->cf.ny = c->nrows;
+    c->have_problem = true;
+    return BURG_OK;
+}
+
+int burg_set_options(burg_ctx *c, int tile_w, int max_passes, double tol, int profile)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (tile_w != 64 && tile_w != 128) return fail(BURG_EINVAL, "tile_w must be 64 or 128");
+    if (!(tol >= 0.0) || !(tol < 1e-6)) return fail(BURG_EINVAL, "tol must be in [0, 1e-6)");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->tw = tile_w;
+    c->max_passes_opt = max_passes;
+    c->tol = tol;
+    c->profile = profile ? 1 : 0;
+    return engine_alloc(c);
+}
+
+int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, double *norm)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w || !wp || !r) return fail(BURG_EINVAL, "null array");
+    if (int e = ensure_scratch(c)) return e;
+    const size_t bytes = c->m() * sizeof(double);
+    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_d, wp, bytes, hipMemcpyHostToDevice, c->stream));
+    double nrm = 0.0;
+    if (int e = residual_norm(c, c->d_x, c->d_d, c->d_r, &nrm)) return e;
+    HIPCHK(hipMemcpyAsync(r, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (norm) *norm = nrm;
+    return BURG_OK;
+}
+
+int burg_jvp(burg_ctx *c, const double *w, const double *x, double *y)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w || !x || !y) return fail(BURG_EINVAL, "null array");
+    if (int e = ensure_scratch(c)) return e;
+    const size_t bytes = c->m() * sizeof(double);
+    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_d, x, bytes, hipMemcpyHostToDevice, c->stream));
+    CHK(launch_jvp(c->cf, c->d_x, c->d_d, c->d_r, c->stream));
+    HIPCHK(hipMemcpyAsync(y, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BURG_OK;
+}
+
+int burg_block_solve(burg_ctx *c, const double *w, const double *rhs, double *delta)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w || !rhs || !delta) return fail(BURG_EINVAL, "null array");
+    if (int e = ensure_scratch(c)) return e;
+    const size_t bytes = c->m() * sizeof(double);
+    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_r, rhs, bytes, hipMemcpyHostToDevice, c->stream));
+    if (int e = block_solve(c, c->d_x, c->d_r, c->d_d)) return e;
+    HIPCHK(hipMemcpyAsync(delta, c->d_d, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BURG_OK;
+}
+
+int burg_upload_state(burg_ctx *c, const double *w)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w) return fail(BURG_EINVAL, "null state");
+    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w, c->m() * sizeof(double),
+                          hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BURG_OK;
+}
+
+int burg_download_state(burg_ctx *c, double *w)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w) return fail(BURG_EINVAL, "null state");
+    HIPCHK(hipMemcpyAsync(w, c->d_state[c->cur], c->m() * sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BURG_OK;
+}
+
+int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (num_steps < 0) return fail(BURG_EINVAL, "num_steps < 0");
+    if (solver != BURG_SOLVER_MARCH && solver != BURG_SOLVER_NEWTON)
+        return fail(BURG_EINVAL, "unknown solver %d", solver);
+    if (st) std::memset(st, 0, sizeof *st);
+    HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream));
+    if (solver == BURG_SOLVER_NEWTON)
+        if (int e = ensure_scratch(c)) return e;
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    int64_t nupd = 0;
+    int maxupd = 0;
+    double rel = 0.0;
+    for (int s = 0; s < num_steps; ++s) {
+        const double *wp = c->d_state[c->cur];
+        double *w = c->d_state[c->cur ^ 1];
+        if (solver == BURG_SOLVER_MARCH) {
+            if (int e = march_step(c, wp, w)) return e;
+        } else {
+            int its = 0;
+            if (int e = newton_step(c, wp, w, 100, 1e-12, &its, &rel)) return e;
+            nupd += its;
+            maxupd = std::max(maxupd, its);
+        }
+        c->cur ^= 1;
+    }
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    if (int e = read_stats(c, st)) return e;
+    if (st) {
+        st->loop_ms = ms;
+        st->newton_updates = nupd;
+        st->newton_max_updates = maxupd;
+        st->last_rel = rel;
+        if (solver == BURG_SOLVER_NEWTON) st->steps = num_steps;
+    }
+    collect_profile(c, st);
+    return BURG_OK;
+}
+
+int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newton_max_its,
+             double newton_rtol, double *snaps, int64_t ld_snaps, int snap_every,
+             burg_stats *st, int32_t *step_iters, double *step_rel)
+{
+    if (int e = check_ready(c)) return e;
+    if (!w0) return fail(BURG_EINVAL, "null w0");
+    if (num_steps < 0) return fail(BURG_EINVAL, "num_steps < 0");
+    if (snap_every < 1) return fail(BURG_EINVAL, "snap_every must be >= 1");
+    if (solver != BURG_SOLVER_MARCH && solver != BURG_SOLVER_NEWTON)
+        return fail(BURG_EINVAL, "unknown solver %d", solver);
+    const int64_t ncols = num_steps / snap_every + 1;
+    if (snaps && ld_snaps < ncols)
+        return fail(BURG_EINVAL, "ld_snaps=%lld < %lld columns", (long long)ld_snaps,
+                    (long long)ncols);
+    if (newton_max_its < 0) return fail(BURG_EINVAL, "newton_max_its < 0");
+    if (st) std::memset(st, 0, sizeof *st);
+    if (int e = ensure_scratch(c)) return e;
+    const size_t m = c->m(), bytes = m * sizeof(double);
+
+    // snapshot chunk: up to S device states, transposed into (m x S) and
+    // copied as a 2D block into columns [col0, col0+S) of the host matrix.
+    int S = 0;
+    double *d_chunk = nullptr, *d_tr = nullptr;
+    bool registered = false;
+    if (snaps) {
+        size_t freeb = 0, totalb = 0;
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        const size_t budget = freeb / 4;
+        S = (int)std::min<int64_t>(ncols, 64);
+        while (S > 1 && (size_t)S * 2 * bytes > budget) S /= 2;
+        if (int e = dalloc(&d_chunk, (size_t)S * m)) return e;
+        if (int e = dalloc(&d_tr, (size_t)S * m)) {
+            dfree(d_chunk);
+            return e;
+        }
+        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
+                                     hipHostRegisterDefault) == hipSuccess;
+        (void)hipGetLastError();
+    }
+    std::vector<const double *> slots;
+    int64_t col0 = 0;
+    float flush_ms = 0.f;
+    hipEvent_t f0 = nullptr, f1 = nullptr;
+    (void)hipEventCreate(&f0);
+    (void)hipEventCreate(&f1);
+    auto flush = [&]() -> int {
+        if (slots.empty()) return 0;
+        HIPCHK(hipEventRecord(f0, c->stream));
+        CHK(launch_transpose(slots.data(), (int)slots.size(), m, d_tr, (int)slots.size(),
+                             c->stream));
+        HIPCHK(hipMemcpy2DAsync(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
+                                slots.size() * sizeof(double), slots.size() * sizeof(double), m,
+                                hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(f1, c->stream));
+        HIPCHK(hipEventSynchronize(f1));
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, f0, f1);
+        flush_ms += t;
+        col0 += (int64_t)slots.size();
+        slots.clear();
+        return 0;
+    };
+    auto keep = [&](const double *state) -> int {
+        double *slot = d_chunk + slots.size() * m;
+        HIPCHK(hipMemcpyAsync(slot, state, bytes, hipMemcpyDeviceToDevice, c->stream));
+        slots.push_back(slot);
+        if ((int)slots.size() == S) return flush();
+        return 0;
+    };
+
+    int rc = BURG_OK;
+    HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, bytes, hipMemcpyHostToDevice, c->stream));
+    if (snaps) rc = keep(c->d_state[c->cur]);
+    int64_t nupd = 0;
+    int maxupd = 0;
+    double rel = 0.0;
+    float loop_ms = 0.f;
+    long long prev_passes = 0;
+    for (int s = 0; s < num_steps && rc == BURG_OK; ++s) {
+        HIPCHK(hipEventRecord(c->ev0, c->stream));
+        const double *wp = c->d_state[c->cur];
+        double *w = c->d_state[c->cur ^ 1];
+        if (solver == BURG_SOLVER_MARCH) {
+            rc = march_step(c, wp, w);
+            if (step_iters && rc == BURG_OK) {
+                // passes of this step = max_passes delta of a one-step stats window
+                DevStats ds{};
+                HIPCHK(hipMemcpyAsync(&ds, c->d_stats, sizeof ds, hipMemcpyDeviceToHost,
+                                      c->stream));
+                HIPCHK(hipStreamSynchronize(c->stream));
+                step_iters[s] = (int32_t)(ds.passes - prev_passes);
+                prev_passes = ds.passes;
+            }
+            if (step_rel) step_rel[s] = 0.0;
+        } else {
+            int its = 0;
+            rc = newton_step(c, wp, w, newton_max_its, newton_rtol, &its, &rel);
+            nupd += its;
+            maxupd = std::max(maxupd, its);
+            if (step_iters) step_iters[s] = its;
+            if (step_rel) step_rel[s] = rel;
+        }
+        HIPCHK(hipEventRecord(c->ev1, c->stream));
+        c->cur ^= 1;
+        if (rc == BURG_OK && snaps && (s + 1) % snap_every == 0) {
+            HIPCHK(hipEventSynchronize(c->ev1));
+            float t = 0.f;
+            (void)hipEventElapsedTime(&t, c->ev0, c->ev1);
+            loop_ms += t;
+            rc = keep(c->d_state[c->cur]);
+        } else if (rc == BURG_OK) {
+            HIPCHK(hipEventSynchronize(c->ev1));
+            float t = 0.f;
+            (void)hipEventElapsedTime(&t, c->ev0, c->ev1);
+            loop_ms += t;
+        }
+    }
+    if (rc == BURG_OK && snaps) rc = flush();
+    if (rc == BURG_OK) rc = read_stats(c, st);
+    if (st) {
+        st->loop_ms = loop_ms;
+        st->flush_ms = flush_ms;
+        st->newton_updates = nupd;
+        st->newton_max_updates = maxupd;
+        st->last_rel = rel;
+        if (solver == BURG_SOLVER_NEWTON) st->steps = num_steps;
+    }
+    collect_profile(c, st);
+    (void)hipStreamSynchronize(c->stream);
+    if (registered) (void)hipHostUnregister(snaps);
+    dfree(d_chunk);
+    dfree(d_tr);
+    (void)hipEventDestroy(f0);
+    (void)hipEventDestroy(f1);
+    if (rc == BURG_OK && st && st->unconverged_steps > 0)
+        return fail(BURG_ENOCONV, "%d steps hit the pass cap", st->unconverged_steps);
+    return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,210 @@
+"""Drop-in host API for the reference FOM hot path (MI355X-backed).
+
+Same names, argument meaning, return layout and error behaviour as the
+reference module ``hypernet2D`` for the FOM path (paths relative to
+/root/reference, C/ = BurgersFD_CleanCoarse/):
+
+  make_2D_grid                  C/hypernet2D.py:2425-2431
+  make_ddx / get_ops            C/hypernet2D.py:2410-2416, 2433-2444 (scipy setup)
+  inviscid_burgers_implicit2D   C/hypernet2D.py:72-131     -> burg_run (HIP)
+  inviscid_burgers_res2D_alt    C/hypernet2D.py:2512-2570  -> burg_residual (HIP)
+  inviscid_burgers_exact_jac2D  C/hypernet2D.py:2627-2656  -> JacobianOperator
+                                (burg_jvp / burg_block_solve, HIP)
+  newton_raphson                C/hypernet2D.py:1811-1857  (host control loop)
+  compute_error                 C/hypernet2D.py:3074-3079
+  param_to_snap_fn              C/hypernet2D.py:3081-3105
+  get_saved_params              C/hypernet2D.py:3107-3109
+  load_or_compute_snaps         C/hypernet2D.py:3111-3145
+
+The snapshot matrix is the reference's: float64, shape (2*nx*ny,
+num_steps + 1), C-contiguous, column j = state after j steps, u rows then v
+rows.  Extensions are keyword-only (solver, snap_every, device, tile_w, tol,
+max_passes, verbose, allow_nonsquare) and default to reference behaviour.
+"""
+import glob
+import os
+import time
+
+import numpy as np
+import scipy.sparse as sp
+from scipy.sparse.linalg import LinearOperator
+
+from .grid import fom_coefficients, make_2D_grid  # noqa: F401  (re-export)
+from .solver import DEFAULT_TOL, get_context
+
+
+def make_ddx(grid_x):
+    """Backward-difference operator (C/hypernet2D.py:2410-2416); setup only."""
+    dx = grid_x[1:] - grid_x[:-1]
+    return sp.spdiags([-np.ones(grid_x.size - 1) / dx, np.ones(grid_x.size - 1) / dx],
+                      [-1, 0], grid_x.size - 1, grid_x.size - 1, "lil")
+
+
+def get_ops(grid_x, grid_y):
+    """(Dxec, Dyec, JDxec, JDyec, Eye) as the reference builds them
+    (C/hypernet2D.py:2433-2444).  Only needed by callers that pass operators
+    around; the HIP path computes the stencil from the grid directly."""
+    Dxec = make_ddx(grid_x)
+    Dyec = make_ddx(grid_y)
+    JDxec = sp.kron(sp.eye(grid_y.size - 1, grid_y.size - 1), Dxec)
+    JDyec = sp.kron(sp.eye(grid_x.size - 1, grid_x.size - 1), Dyec)
+    JDyec = JDyec.tocsr()
+    idx = np.arange((grid_y.size - 1) * (grid_x.size - 1)).reshape(
+        (grid_y.size - 1, grid_x.size - 1)).T.ravel()
+    JDyec = JDyec[idx, :]
+    JDyec = JDyec[:, idx]
+    Eye = sp.identity(2 * (grid_x.size - 1) * (grid_y.size - 1))
+    return Dxec, Dyec, JDxec, JDyec, Eye
+
+
+def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
+    nx, ny = np.asarray(grid_x).size - 1, np.asarray(grid_y).size - 1
+    ctx = get_context(nx, ny, device, **opts)
+    ctx.set_problem(grid_x, grid_y, dt, mu, allow_nonsquare)
+    return ctx
+
+
+def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
+                                snap_every=1, device=0, tile_w=64, tol=DEFAULT_TOL,
+                                max_passes=0, verbose=1, allow_nonsquare=False,
+                                newton_max_its=100, newton_rtol=1e-12, return_stats=False):
+    """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM
+    (C/hypernet2D.py:72-131) on an MI355X.
+
+    solver="march" (default) solves each implicit step exactly with the
+    closed-form upwind march; solver="newton" runs the reference algorithm
+    (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
+    Both return the reference's snapshot matrix.  verbose=1 prints the
+    reference's header line; verbose=2 also the per-step lines
+    (" ... Working on timestep i" and Newton's "k: rel").
+    """
+    if verbose:
+        print("Running HDM for mu1={}".format(mu[0]))
+    ctx = _ctx_for(grid_x, grid_y, dt, mu, device, allow_nonsquare, tile_w=tile_w,
+                   max_passes=max_passes, tol=tol)
+    snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
+                                     solver, newton_max_its, newton_rtol, int(snap_every))
+    if verbose >= 2:
+        for i in range(int(num_steps)):
+            print(" ... Working on timestep {}".format(i))
+            if solver == "newton":
+                print("{}: {:3.2e}".format(its[i], rel[i]))
+    if return_stats:
+        stats = dict(stats, step_iters=its, step_rel=rel)
+        return snaps, stats
+    return snaps
+
+
+def inviscid_burgers_res2D_alt(w, grid_x, grid_y, dt, wp, mu, JDxec=None, JDyec=None, *,
+                               device=0):
+    """FOM residual R(w; wp, mu) (C/hypernet2D.py:2512-2570), computed on the GPU.
+    JDxec/JDyec are accepted for signature compatibility and ignored."""
+    ctx = _ctx_for(grid_x, grid_y, dt, mu, device)
+    r, _ = ctx.residual(w, wp)
+    return r
+
+
+class JacobianOperator(LinearOperator):
+    """J(w) of inviscid_burgers_exact_jac2D (C/hypernet2D.py:2627-2656) as a
+    matrix-free operator: ``J @ x`` runs the HIP Jacobian-vector kernel and
+    ``J.solve(b)`` the exact block forward substitution (what spsolve(J, b)
+    computes at :1854)."""
+
+    def __init__(self, ctx, w):
+        self._ctx = ctx
+        self._w = np.ascontiguousarray(np.asarray(w, dtype=np.float64).ravel())
+        super().__init__(dtype=np.float64, shape=(ctx.m, ctx.m))
+
+    def _matvec(self, x):
+        return self._ctx.jvp(self._w, np.asarray(x, dtype=np.float64).ravel())
+
+    def solve(self, b):
+        return self._ctx.block_solve(self._w, np.asarray(b, dtype=np.float64).ravel())
+
+
+def _grid_from_ops(JDxec, JDyec, n):
+    nx = int(round(np.sqrt(n)))
+    if nx * nx != n:
+        raise ValueError("pass grid_x/grid_y for a non-square grid")
+    inv_dx = np.asarray(JDxec.diagonal()[:nx], dtype=np.float64)
+    inv_dy = np.asarray(JDyec.diagonal()[::nx][:nx], dtype=np.float64)
+    gx = np.concatenate(([0.0], np.cumsum(1.0 / inv_dx)))
+    gy = np.concatenate(([0.0], np.cumsum(1.0 / inv_dy)))
+    return gx, gy
+
+
+def inviscid_burgers_exact_jac2D(w, dt, JDxec=None, JDyec=None, Eye=None, *, grid_x=None,
+                                 grid_y=None, device=0):
+    """Exact FOM Jacobian at w (C/hypernet2D.py:2627-2656) as a JacobianOperator.
+    The grid comes from grid_x/grid_y, or is recovered from JDxec/JDyec."""
+    w = np.asarray(w, dtype=np.float64).ravel()
+    if grid_x is None or grid_y is None:
+        grid_x, grid_y = _grid_from_ops(JDxec, JDyec, w.size // 2)
+    # the Jacobian does not depend on mu or the source: any mu is fine here
+    ctx = _ctx_for(grid_x, grid_y, dt, (1.0, 0.0), device)
+    return JacobianOperator(ctx, w)
+
+
+def newton_raphson(func, jac, x0, max_its=20, relnorm_cutoff=1e-12):
+    """newton_raphson (C/hypernet2D.py:1811-1857) with the reference's control
+    flow and print line.  The linear solve uses J.solve(f) when J is a
+    JacobianOperator (HIP exact block solve), else scipy's spsolve as the
+    reference does."""
+    x = np.array(x0, dtype=np.float64, copy=True)
+    init_norm = np.linalg.norm(func(x0))
+    resnorms = []
+    for i in range(max_its):
+        resnorm = np.linalg.norm(func(x))
+        resnorms.append(resnorm)
+        if resnorm / init_norm < relnorm_cutoff:
+            print("{}: {:3.2e}".format(i, resnorm / init_norm))
+            break
+        J = jac(x)
+        f = func(x)
+        if hasattr(J, "solve"):
+            x -= J.solve(f)
+        else:
+            x -= sp.linalg.spsolve(J, f)
+    return x, resnorms
+
+
+def compute_error(rom_snaps, hdm_snaps):
+    """Relative error at each time step (C/hypernet2D.py:3074-3079)."""
+    sq_hdm = np.sqrt(np.square(rom_snaps).sum(axis=0))
+    sq_err = np.sqrt(np.square(rom_snaps - hdm_snaps).sum(axis=0))
+    rel_err = sq_err / sq_hdm
+    return rel_err, rel_err.mean()
+
+
+def param_to_snap_fn(mu, snap_folder="param_snaps", suffix=".npy"):
+    """'param_snaps/mu1_{mu1}+mu2_{mu2}.npy' (C/hypernet2D.py:3081-3105)."""
+    snapfn = snap_folder + "/"
+    for i in range(len(mu)):
+        if i > 0:
+            snapfn += "+"
+        snapfn += "mu{}_{}".format(i + 1, mu[i])
+    return snapfn + suffix
+
+
+def get_saved_params(snap_folder="param_snaps"):
+    """Set of cached snapshot files (C/hypernet2D.py:3107-3109)."""
+    return set(glob.glob(snap_folder + "/*"))
+
+
+def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="param_snaps",
+                          **solver_kw):
+    """Load cached snapshots for mu, or compute and cache them
+    (C/hypernet2D.py:3111-3145).  solver_kw go to inviscid_burgers_implicit2D."""
+    if not os.path.exists(snap_folder):
+        os.makedirs(snap_folder)
+    snap_fn = param_to_snap_fn(mu, snap_folder=snap_folder)
+    if snap_fn in get_saved_params(snap_folder=snap_folder):
+        print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
+        snaps = np.load(snap_fn)[:, :num_steps + 1]
+    else:
+        print(f"Computing new snaps for mu1={mu[0]}, mu2={mu[1]}")
+        t0 = time.time()
+        snaps = inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, **solver_kw)
+        print("Elapsed time: {:3.3e}".format(time.time() - t0))
+        np.save(snap_fn, snaps)
+    return snaps

@@ -1,0 +1,144 @@
+"""Context object over libburgers_hip: one grid on one MI355X.
+
+FOMContext owns a ``burg_ctx`` (device buffers, HIP stream).  It is the only
+place the package calls into the C ABI; hypernet2D.py / run_fom.py build the
+reference-compatible API on top of it.
+"""
+import ctypes
+import threading
+import warnings
+
+import numpy as np
+
+from . import _lib
+from .grid import fom_coefficients
+
+DEFAULT_TOL = 2.0 ** -50  # 4 ulp relative inflow motion
+
+
+class FOMContext:
+    """A grid (nx x ny) resident on one GPU."""
+
+    def __init__(self, nx, ny, device=0, tile_w=64, max_passes=0, tol=DEFAULT_TOL,
+                 profile=False):
+        self._L = _lib.load()
+        self.nx, self.ny, self.device = int(nx), int(ny), int(device)
+        h = ctypes.c_void_p()
+        _lib.check(self._L.burg_ctx_create(self.device, self.nx, self.ny, ctypes.byref(h)))
+        self._h = h
+        self._problem = None
+        self.set_options(tile_w, max_passes, tol, profile)
+
+    @property
+    def m(self):
+        return 2 * self.nx * self.ny
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.burg_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_options(self, tile_w=64, max_passes=0, tol=DEFAULT_TOL, profile=False):
+        _lib.check(self._L.burg_set_options(self._h, int(tile_w), int(max_passes), float(tol),
+                                            1 if profile else 0))
+        self.options = dict(tile_w=tile_w, max_passes=max_passes, tol=tol, profile=profile)
+
+    def set_problem(self, grid_x, grid_y, dt, mu, allow_nonsquare=False):
+        key = (np.asarray(grid_x).tobytes(), np.asarray(grid_y).tobytes(), float(dt),
+               float(mu[0]), float(mu[1]), bool(allow_nonsquare))
+        if key == self._problem:
+            return
+        ix, iy, src, lbc = fom_coefficients(grid_x, grid_y, dt, mu, allow_nonsquare)
+        if ix.size != self.nx or iy.size != self.ny:
+            raise ValueError("grid does not match the context shape")
+        _lib.check(self._L.burg_set_problem(self._h, _lib.dptr(ix), _lib.dptr(iy),
+                                            _lib.dptr(src), _lib.dptr(lbc), float(dt)))
+        self._problem = key
+
+    def _vec(self, a, name):
+        a = np.ascontiguousarray(np.asarray(a, dtype=np.float64).ravel())
+        if a.size != self.m:
+            raise ValueError(f"{name} has {a.size} entries, expected {self.m}")
+        return a
+
+    # ---- parity hooks -----------------------------------------------------
+    def residual(self, w, wp):
+        w, wp = self._vec(w, "w"), self._vec(wp, "wp")
+        r = np.empty(self.m)
+        nrm = ctypes.c_double()
+        _lib.check(self._L.burg_residual(self._h, _lib.dptr(w), _lib.dptr(wp), _lib.dptr(r),
+                                         ctypes.byref(nrm)))
+        return r, nrm.value
+
+    def jvp(self, w, x):
+        w, x = self._vec(w, "w"), self._vec(x, "x")
+        y = np.empty(self.m)
+        _lib.check(self._L.burg_jvp(self._h, _lib.dptr(w), _lib.dptr(x), _lib.dptr(y)))
+        return y
+
+    def block_solve(self, w, rhs):
+        w, rhs = self._vec(w, "w"), self._vec(rhs, "rhs")
+        d = np.empty(self.m)
+        _lib.check(self._L.burg_block_solve(self._h, _lib.dptr(w), _lib.dptr(rhs),
+                                            _lib.dptr(d)))
+        return d
+
+    # ---- time loop --------------------------------------------------------
+    def run(self, w0, num_steps, solver="march", newton_max_its=100, newton_rtol=1e-12,
+            snap_every=1, keep_snaps=True):
+        """Returns (snaps (m, num_steps//snap_every + 1) C-order or None,
+        stats dict, per-step iterations int32[num_steps], per-step rel[num_steps])."""
+        w0 = self._vec(w0, "w0")
+        ncols = num_steps // snap_every + 1
+        snaps = np.zeros((self.m, ncols)) if keep_snaps else None
+        its = np.zeros(num_steps, dtype=np.int32)
+        rel = np.zeros(num_steps)
+        st = _lib.BurgStats()
+        code = self._L.burg_run(self._h, _lib.dptr(w0), int(num_steps), _lib.SOLVERS[solver],
+                                int(newton_max_its), float(newton_rtol),
+                                _lib.dptr(snaps), ncols, int(snap_every), ctypes.byref(st),
+                                _lib.iptr(its), _lib.dptr(rel))
+        _lib.check(code, allow=(_lib.BURG_ENOCONV,))
+        if code == _lib.BURG_ENOCONV:
+            warnings.warn(self._L.burg_last_error().decode(), _lib.NotConvergedWarning)
+        return snaps, st.as_dict(), its, rel
+
+    def upload(self, w):
+        w = self._vec(w, "w")
+        _lib.check(self._L.burg_upload_state(self._h, _lib.dptr(w)))
+
+    def download(self):
+        w = np.empty(self.m)
+        _lib.check(self._L.burg_download_state(self._h, _lib.dptr(w)))
+        return w
+
+    def advance(self, num_steps, solver="march"):
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_advance(self._h, int(num_steps), _lib.SOLVERS[solver],
+                                        ctypes.byref(st)), allow=())
+        return st.as_dict()
+
+
+_cache = threading.local()
+
+
+def get_context(nx, ny, device=0, **opts):
+    """Per-thread cached context for (device, nx, ny); options re-applied."""
+    d = getattr(_cache, "ctxs", None)
+    if d is None:
+        d = _cache.ctxs = {}
+    key = (int(device), int(nx), int(ny))
+    ctx = d.get(key)
+    if ctx is None:
+        ctx = d[key] = FOMContext(nx, ny, device, **opts)
+    elif opts and any(ctx.options.get(k) != v for k, v in opts.items()):
+        merged = dict(ctx.options)
+        merged.update(opts)
+        ctx.set_options(**merged)
+    return ctx

@@ -1,0 +1,141 @@
+/*
+ * burgers.h -- C ABI of libburgers_hip.so, the MI355X (gfx950) implementation
+ * of the SADPR/FiniteDifference full-order-model (FOM) hot path.
+ *
+ * Reference interfaces replaced (paths relative to /root/reference,
+ * C/ = BurgersFD_CleanCoarse/).  The reference has no FFI: every entry point
+ * below replaces a Python function and is bound with ctypes by
+ * finitedifference_amd/_lib.py (binding stub in INTEGRATION.md).
+ *
+ *   burg_run            C/hypernet2D.py:72-131   inviscid_burgers_implicit2D
+ *                       (time loop + snapshot matrix), including
+ *                       C/hypernet2D.py:1811-1857 newton_raphson and
+ *                       C/hypernet2D.py:1854      spsolve, which it replaces
+ *   burg_residual       C/hypernet2D.py:2512-2570 inviscid_burgers_res2D_alt
+ *                       (+ np.linalg.norm of it, :1831/:1839)
+ *   burg_jvp            C/hypernet2D.py:2627-2656 inviscid_burgers_exact_jac2D(w) @ x
+ *   burg_block_solve    C/hypernet2D.py:1854      spsolve(J(w), rhs)
+ *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
+ *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
+ *
+ * Conventions
+ *   - State w has 2*nx*ny doubles: [u.ravel(), v.ravel()], u row-major
+ *     (ny, nx), cell (r, c) at r*nx + c (C/run_fom.py:33-35).
+ *   - All pointers passed in are HOST pointers owned by the caller and
+ *     borrowed for the duration of the call; the library keeps none of them.
+ *   - Every function returns BURG_OK (0) or a negative BURG_E* code; the
+ *     message of the last failure on the calling thread is burg_last_error().
+ *   - One context per host thread; a context owns its device buffers,
+ *     its HIP stream and (multi-GPU) its RCCL communicator.
+ */
+#ifndef BURGERS_H
+#define BURGERS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BURG_ABI_VERSION 1
+
+enum burg_status {
+    BURG_OK = 0,
+    BURG_EINVAL = -1,   /* bad argument (null pointer, size, option) */
+    BURG_ESHAPE = -2,   /* grid shape not supported (e.g. nx != ny in strict mode) */
+    BURG_EHIP = -3,     /* HIP runtime error */
+    BURG_ERCCL = -4,    /* RCCL error */
+    BURG_ENOMEM = -5,   /* device or pinned-host allocation failed */
+    BURG_ENOCONV = -6,  /* solver hit its iteration cap (result still returned) */
+    BURG_ENAN = -7,     /* non-finite residual or state */
+    BURG_ESTATE = -8    /* call order error (e.g. run before set_problem) */
+};
+
+enum burg_solver {
+    BURG_SOLVER_MARCH = 0,  /* closed-form upwind march (default, exact implicit step) */
+    BURG_SOLVER_NEWTON = 1  /* newton_raphson + exact block solve (reference algorithm) */
+};
+
+typedef struct burg_ctx burg_ctx;
+
+typedef struct burg_stats {
+    int64_t steps;              /* time steps advanced */
+    int64_t tile_marches;       /* tiles marched (all Jacobi passes, all steps) */
+    int64_t passes;             /* march launches that did work */
+    int32_t max_passes;         /* most passes one step needed (incl. the confirming one) */
+    int32_t unconverged_steps;  /* steps that hit the pass cap; 0 on success */
+    int64_t newton_updates;     /* newton solver: total Newton updates */
+    int32_t newton_max_updates; /* newton solver: most updates in one step */
+    int32_t reserved;
+    double loop_ms;             /* device time of the time loop (HIP events) */
+    double flush_ms;            /* device time of snapshot transpose + D2H */
+    double march_kernel_ms;     /* profiling mode: summed march kernel time */
+    int64_t march_launches;     /* profiling mode: march kernel launches timed */
+    double last_rel;            /* newton solver: last step's final ||R||/||R0|| */
+} burg_stats;
+
+int burg_abi_version(void);
+const char *burg_last_error(void);
+
+/* Create a context on HIP device `device` for an nx x ny grid (single GPU). */
+int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);
+
+/* Multi-GPU: this rank owns global rows [row0, row0 + nrows) of an
+ * nx x ny_total grid.  `nccl_id` points to a 128-byte ncclUniqueId made by
+ * rank 0 (burg_rccl_unique_id) and broadcast by the caller.  world == 1
+ * behaves as burg_ctx_create. */
+int burg_rccl_unique_id(void *id_out_128_bytes);
+int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows,
+                         int rank, int world, const void *nccl_id, burg_ctx **out);
+
+void burg_ctx_destroy(burg_ctx *ctx);
+
+/* Problem data, computed by the caller exactly as NumPy does in the reference
+ * (GLOBAL arrays; a slab context picks its rows):
+ *   inv_dx[nx]        = 1/dx_c              (make_ddx, C/hypernet2D.py:2414)
+ *   inv_dy[ny_total]  = 1/dy_r
+ *   src[nx]           = dt*0.02*exp(mu2*xc) (:2550)
+ *   lbc[ny_total]     = 0.5*dt*mu1**2/dx[r] (:2553-2554, row-indexed quirk)  */
+int burg_set_problem(burg_ctx *ctx, const double *inv_dx, const double *inv_dy,
+                     const double *src, const double *lbc, double dt);
+
+/* Engine options.  tile_w: tile width in cells (64 or 128; tile height is the
+ * 64-lane wavefront).  max_passes: Jacobi pass cap per step (<= 0: the
+ * guaranteed bound, #tile anti-diagonals + 1).  tol: relative inflow change
+ * below which a tile is not re-marched (0 = bitwise fixed point).
+ * profile: 1 = time every march launch with HIP events (burg_stats). */
+int burg_set_options(burg_ctx *ctx, int tile_w, int max_passes, double tol, int profile);
+
+/* Parity hooks (whole-grid host arrays; single-GPU contexts only). */
+int burg_residual(burg_ctx *ctx, const double *w, const double *wp, double *r,
+                  double *norm_out);
+int burg_jvp(burg_ctx *ctx, const double *w, const double *x, double *y);
+int burg_block_solve(burg_ctx *ctx, const double *w, const double *rhs, double *delta);
+
+/* Time loop (inviscid_burgers_implicit2D).  w0: this context's rows of the
+ * initial state (2*nx*nrows).  snaps: C-order host matrix with leading
+ * dimension ld_snaps (>= num_steps/snap_every + 1); column j receives the
+ * state after j*snap_every steps, rows as in w (u rows then v rows of this
+ * context).  snaps may be NULL (no snapshots kept).  solver: burg_solver.
+ * newton_max_its / newton_rtol: newton_raphson's max_its / relnorm_cutoff.
+ * step_iters[num_steps] / step_rel[num_steps] (each may be NULL): per step,
+ * the Newton update count and final ||R||/||R(wp)|| (newton solver; the
+ * numbers newton_raphson prints, C/hypernet2D.py:1844), or the march passes
+ * and 0.0 (march solver). */
+int burg_run(burg_ctx *ctx, const double *w0, int num_steps, int solver,
+             int newton_max_its, double newton_rtol, double *snaps,
+             int64_t ld_snaps, int snap_every, burg_stats *stats,
+             int32_t *step_iters, double *step_rel);
+
+/* Device-resident stepping for benchmarks: upload once, advance, download.
+ * burg_advance keeps the state in HBM (no host traffic) and waits for the
+ * device before returning; stats->loop_ms is its device time. */
+int burg_upload_state(burg_ctx *ctx, const double *w);
+int burg_advance(burg_ctx *ctx, int num_steps, int solver, burg_stats *stats);
+int burg_download_state(burg_ctx *ctx, double *w);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BURGERS_H */

@@ -301,3 +301,169 @@ int orc_fom(int nx, int ny, const double *inv_dx, const double *inv_dy,
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Schedule simulator for the HIP tile engine (test support, not a reference
+ * restatement).  The grid is cut into th x tw tiles that are all marched in
+ * parallel per iteration (block Jacobi over tiles).  Iteration 1 guesses each
+ * interior tile inflow from wp ("the neighbour did not move"); iteration k>1
+ * re-marches a tile only if one of its inflow values moved by more than
+ * tol*|value| away from the inflow the tile last used.  Stops when no tile
+ * was re-marched.  tol = 0 demands the bitwise fixed point, which equals the
+ * sequential march but needs O(#tile rows) iterations in y-uniform regions
+ * (1-ulp fixed points of the rounded recurrence); a few ulps suffice for
+ * the iteration to stop after 2-4 passes.
+ * Returns iterations run; *tiles_done = tiles marched.                      */
+typedef struct {
+    const double *inv_dx, *inv_dy, *src, *lbc;
+    double a;
+    int nx, ny;
+} orc_grid;
+
+static inline void cell_pre(const orc_grid *g, int r, int c, double pu, double pv,
+                            double *bu, double *bv, double *xfp, double *xhp,
+                            double *yhp, double *ygp)
+{
+    const double ax = g->a * g->inv_dx[c], ay = g->a * g->inv_dy[r];
+    const double sl = c == 0 ? g->src[0] + g->lbc[r] : g->src[c];
+    const double hu = 0.5 * pu;
+    *xfp = ax * (hu * pu);
+    *xhp = ax * (hu * pv);
+    *yhp = ay * (hu * pv);
+    *ygp = ay * ((0.5 * pv) * pv);
+    *bu = ((pu - *xfp) - *yhp) + sl;
+    *bv = (pv - *ygp) - *xhp;
+}
+
+static inline int moved(double a, double b, double tol)
+{
+    const double d = fabs(a - b), m = fmax(fabs(a), fabs(b));
+    return tol == 0.0 ? a != b : d > tol * m;
+}
+
+int orc_march_tiled_sim(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                        const double *src, const double *lbc, double dt,
+                        const double *wp, double *w, int th, int tw, int kmax,
+                        double tol, long long *tiles_done)
+{
+    const size_t n = (size_t)nx * ny;
+    const int nti = (ny + th - 1) / th, ntj = (nx + tw - 1) / tw;
+    const size_t nt = (size_t)nti * ntj;
+    orc_grid g = {inv_dx, inv_dy, src, lbc, 0.5 * dt, nx, ny};
+    /* current outflow edges: E (xf, xh) per tile row, N (yh, yg) per tile column;
+     * used inflows: W (xf, xh) and S (yh, yg) as last marched with            */
+    double *E = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *Nn = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *E2 = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *N2 = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *Wu = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *Su = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *yh = (double *)malloc(tw * sizeof(double)), *yg = (double *)malloc(tw * sizeof(double));
+    double *win = (double *)malloc(2 * th * sizeof(double)), *sin_ = (double *)malloc(2 * tw * sizeof(double));
+    long long done = 0;
+    int k;
+    for (k = 1; k <= kmax; ++k) {
+        int any = 0;
+        memcpy(E2, E, nt * 2 * th * sizeof(double));
+        memcpy(N2, Nn, nt * 2 * tw * sizeof(double));
+        for (int I = 0; I < nti; ++I)
+            for (int J = 0; J < ntj; ++J) {
+                const size_t t = (size_t)I * ntj + J;
+                const int r0 = I * th, c0 = J * tw;
+                const int r1 = r0 + th < ny ? r0 + th : ny, c1 = c0 + tw < nx ? c0 + tw : nx;
+                /* gather inflow */
+                for (int c = c0; c < c1; ++c) {
+                    double sh = 0.0, sg = 0.0;
+                    if (I > 0) {
+                        if (k == 1) {
+                            double bu, bv, xfp, xhp, yhp, ygp;
+                            const size_t i = IDX(r0 - 1, c, nx);
+                            const double pu = wp[i], pv = wp[n + i];
+                            cell_pre(&g, r0 - 1, c, pu, pv, &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                            const double hy = 0.5 * (g.a * inv_dy[r0 - 1]);
+                            sh = fma(hy * pu, pv, yhp);
+                            sg = fma(hy * pv, pv, ygp);
+                        } else {
+                            const double *sn = N2 + (t - ntj) * 2 * tw;
+                            sh = sn[c - c0];
+                            sg = sn[tw + c - c0];
+                        }
+                    }
+                    sin_[c - c0] = sh;
+                    sin_[tw + c - c0] = sg;
+                }
+                for (int r = r0; r < r1; ++r) {
+                    double xf = 0.0, xh = 0.0;
+                    if (J > 0) {
+                        if (k == 1) {
+                            double bu, bv, xfp, xhp, yhp, ygp;
+                            const size_t i = IDX(r, c0 - 1, nx);
+                            const double pu = wp[i], pv = wp[n + i];
+                            cell_pre(&g, r, c0 - 1, pu, pv, &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                            const double hx = 0.5 * (g.a * inv_dx[c0 - 1]);
+                            xf = fma(hx * pu, pu, xfp);
+                            xh = fma(hx * pu, pv, xhp);
+                        } else {
+                            const double *se = E2 + (t - 1) * 2 * th;
+                            xf = se[r - r0];
+                            xh = se[th + r - r0];
+                        }
+                    }
+                    win[r - r0] = xf;
+                    win[th + r - r0] = xh;
+                }
+                int need = (k == 1);
+                if (!need) {
+                    double *wu = Wu + t * 2 * th, *su = Su + t * 2 * tw;
+                    for (int r = 0; r < r1 - r0 && !need; ++r)
+                        need = moved(win[r], wu[r], tol) || moved(win[th + r], wu[th + r], tol);
+                    for (int c = 0; c < c1 - c0 && !need; ++c)
+                        need = moved(sin_[c], su[c], tol) || moved(sin_[tw + c], su[tw + c], tol);
+                }
+                if (!need) continue;
+                any = 1;
+                ++done;
+                memcpy(Wu + t * 2 * th, win, 2 * th * sizeof(double));
+                memcpy(Su + t * 2 * tw, sin_, 2 * tw * sizeof(double));
+                for (int c = c0; c < c1; ++c) {
+                    yh[c - c0] = sin_[c - c0];
+                    yg[c - c0] = sin_[tw + c - c0];
+                }
+                double *eo = E + t * 2 * th, *no = Nn + t * 2 * tw;
+                for (int r = r0; r < r1; ++r) {
+                    double xfw = win[r - r0], xhw = win[th + r - r0];
+                    const double ay = g.a * inv_dy[r], hy = 0.5 * ay;
+                    for (int c = c0; c < c1; ++c) {
+                        const size_t i = IDX(r, c, nx);
+                        const double hx = 0.5 * (g.a * inv_dx[c]);
+                        double bu, bv, xfp, xhp, yhp, ygp;
+                        cell_pre(&g, r, c, wp[i], wp[n + i], &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                        const double cu = (bu + xfw) + yh[c - c0];
+                        const double cv = (bv + yg[c - c0]) + xhw;
+                        const double mm = fma(hx, cu, hy * cv);
+                        const double s = 0.5 + sqrt(0.25 + mm);
+                        const double rs = 1.0 / s;
+                        const double nu = cu * rs, nv = cv * rs;
+                        const double hxu = hx * nu;
+                        xfw = fma(hxu, nu, xfp);
+                        xhw = fma(hxu, nv, xhp);
+                        yh[c - c0] = fma(hy * nu, nv, yhp);
+                        yg[c - c0] = fma(hy * nv, nv, ygp);
+                        w[i] = nu;
+                        w[n + i] = nv;
+                    }
+                    eo[r - r0] = xfw;
+                    eo[th + r - r0] = xhw;
+                }
+                for (int c = c0; c < c1; ++c) {
+                    no[c - c0] = yh[c - c0];
+                    no[tw + c - c0] = yg[c - c0];
+                }
+            }
+        if (!any) break;
+    }
+    free(E); free(Nn); free(E2); free(N2); free(Wu); free(Su);
+    free(yh); free(yg); free(win); free(sin_);
+    if (tiles_done) *tiles_done = done;
+    return k;
+}

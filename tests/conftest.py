@@ -1,0 +1,36 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs under gpurun)")
+    config.addinivalue_line("markers", "slow: longer CPU-side oracle runs")
+
+
+def golden(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+@pytest.fixture(scope="session")
+def orc():
+    from oracle import oracle
+    oracle.lib()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def gpu():
+    """Skip-free GPU gate: a gpu-marked test fails loudly if the HIP library or
+    the device is missing (no silent fallback)."""
+    import torch  # noqa: F401  (device plumbing only; import checks ROCm runtime)
+    from finitedifference_amd import _lib
+    _lib.load()
+    return _lib

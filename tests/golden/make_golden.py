@@ -1,0 +1,264 @@
+"""Generate the golden fixtures in tests/golden/ from the Python reference.
+
+Runs ONLY in the build container, where /root/reference exists; the fixtures
+(small .npz/.json files: inputs and reference outputs, no reference source)
+are committed and travel to the GPU box instead of the reference.
+
+Recipe: PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg
+OPENBLAS_NUM_THREADS=1, reference on sys.path, scratch cwd (the reference's
+load_or_compute_snaps writes param_snaps/ into the cwd).
+
+    python tests/golden/make_golden.py [--skip-750] [--coarse-npy PATH]
+
+Fixtures written
+  ref_small.npz      full reference trajectories (inviscid_burgers_implicit2D,
+                     C/hypernet2D.py:72) at small square grids + Newton
+                     update counts and printed relative residuals per step
+  ref_ops.npz        single-call residual (res2D_alt, :2512), Jacobian action
+                     (exact_jac2D @ x, :2627) and spsolve(J, r) (:1854) at
+                     random states, seed 1234557 (C/config.py:12)
+  ref_coarse250.npz  C/run_fom.py:main() defaults (250^2, 500 steps,
+                     mu=(5.19, 0.026)): slices, column norms/sums, full
+                     states at steps 1/100/500, Newton counts
+  ref_fine750.npz    F/ grid 750^2, first 2 steps at mu=(5.19, 0.026)
+  author_pickles.npz HDM mid-line slices byte-scanned (never unpickled) from
+                     the author's C/ and F/ predict_mu_5.19e+00_2.60e-02_hprom.pickle
+  author_logs.json   Newton counts/residuals from the author's SLURM log
+                     F/output_55034725.log (750^2)
+"""
+import argparse
+import contextlib
+import io
+import json
+import os
+import pickletools
+import re
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REF = "/root/reference"
+COARSE = os.path.join(REF, "BurgersFD_CleanCoarse")
+FINE = os.path.join(REF, "BurgersFD_CleanFine")
+HERE = os.path.dirname(os.path.abspath(__file__))
+NEWTON_RE = re.compile(r"^(\d+): ([0-9.eE+-]+)\s*$")
+SEED = 1234557  # C/config.py:12
+
+
+def _import_reference():
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, COARSE)
+    import hypernet2D  # noqa: E402  (reference module, build container only)
+    return hypernet2D
+
+
+def _newton_log(text):
+    its, rel = [], []
+    for line in text.splitlines():
+        m = NEWTON_RE.match(line.strip())
+        if m:
+            its.append(int(m.group(1)))
+            rel.append(float(m.group(2)))
+    return np.array(its, dtype=np.int32), np.array(rel)
+
+
+def run_reference(hn, N, T, mu, dt=0.05):
+    gx, gy = hn.make_2D_grid(0, 100, 0, 100, N, N)
+    w0 = np.ones(2 * N * N)
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        snaps = hn.inviscid_burgers_implicit2D(gx, gy, w0, dt, T, list(mu))
+    its, rel = _newton_log(buf.getvalue())
+    assert its.size == T, (its.size, T)
+    return snaps, its, rel
+
+
+def make_small(hn):
+    out = {}
+    cases = [  # (tag, N, T, mu)
+        ("n8", 8, 500, (5.19, 0.026)),
+        ("n13", 13, 40, (5.19, 0.026)),
+        ("n16", 16, 100, (5.19, 0.026)),
+        ("n16b", 16, 60, (4.56, 0.019)),
+        ("n50", 50, 20, (4.75, 0.02)),
+        ("n100", 100, 6, (5.19, 0.026)),
+    ]
+    for tag, N, T, mu in cases:
+        t = time.time()
+        snaps, its, rel = run_reference(hn, N, T, mu)
+        out[f"{tag}_snaps"] = snaps
+        out[f"{tag}_its"] = its
+        out[f"{tag}_rel"] = rel
+        out[f"{tag}_meta"] = np.array([N, T, mu[0], mu[1], 0.05])
+        print(f"small {tag}: N={N} T={T} {time.time() - t:.1f}s its={its[:6]}")
+    np.savez_compressed(os.path.join(HERE, "ref_small.npz"), **out)
+
+
+def make_ops(hn):
+    import scipy.sparse.linalg as spla
+    rng = np.random.default_rng(SEED)
+    out = {}
+    for N in (16, 64, 250):
+        gx, gy = hn.make_2D_grid(0, 100, 0, 100, N, N)
+        _, _, JDxec, JDyec, Eye = hn.get_ops(gx, gy)
+        mu = [4.25 + 1.25 * rng.random(), 0.015 + 0.015 * rng.random()]
+        dt = 0.05
+        w = rng.uniform(1.0, 6.0, 2 * N * N)
+        wp = rng.uniform(1.0, 6.0, 2 * N * N)
+        x = rng.standard_normal(2 * N * N)
+        r = hn.inviscid_burgers_res2D_alt(w, gx, gy, dt, wp, mu, JDxec, JDyec)
+        J = hn.inviscid_burgers_exact_jac2D(w, dt, JDxec, JDyec, Eye)
+        jx = J @ x
+        r1 = hn.inviscid_burgers_res2D(w, gx, gy, dt, wp, mu,
+                                       hn.make_ddx(gx), hn.make_ddx(gy))
+        tag = f"n{N}"
+        out[f"{tag}_mu"] = np.array(mu)
+        if N <= 64:
+            d = spla.spsolve(J.tocsc(), r)
+            out.update({f"{tag}_w": w, f"{tag}_wp": wp, f"{tag}_x": x,
+                        f"{tag}_res": r, f"{tag}_res1d": r1, f"{tag}_jx": jx,
+                        f"{tag}_solve": d})
+        else:  # 250^2: regenerate inputs from the seed in the test; keep summaries
+            idx = rng.choice(2 * N * N, 512, replace=False)
+            out.update({f"{tag}_w": w, f"{tag}_wp": wp, f"{tag}_x": x,
+                        f"{tag}_res_norm": np.linalg.norm(r),
+                        f"{tag}_res_idx": idx, f"{tag}_res_at": r[idx],
+                        f"{tag}_jx_norm": np.linalg.norm(jx), f"{tag}_jx_at": jx[idx]})
+        print(f"ops N={N} done")
+    np.savez_compressed(os.path.join(HERE, "ref_ops.npz"), **out)
+
+
+def _summaries(snaps, N, steps_full):
+    n = N * N
+    T1 = snaps.shape[1]
+    mid = N // 2
+    every = np.arange(0, T1, 10)
+    U = snaps[:n, every].reshape(N, N, -1)
+    V = snaps[n:, every].reshape(N, N, -1)
+    out = {
+        "slice_steps": every,
+        "u_row": U[mid, :, :].T.copy(), "u_col": U[:, mid, :].T.copy(),
+        "v_row": V[mid, :, :].T.copy(), "v_col": V[:, mid, :].T.copy(),
+        "col_norm": np.sqrt(np.square(snaps).sum(axis=0)),
+        "col_sum": snaps.sum(axis=0),
+    }
+    for j in steps_full:
+        if j < T1:
+            out[f"state_{j}"] = snaps[:, j].copy()
+    return out
+
+
+def make_coarse250(hn, coarse_npy=None, coarse_log=None):
+    N, T = 250, 500
+    if coarse_npy and os.path.exists(coarse_npy):
+        # cached output of this same recipe (C/run_fom.py main(), 623 s here)
+        snaps = np.load(coarse_npy, mmap_mode="r")
+        its, rel = _newton_log(open(coarse_log).read())
+        print("coarse250: using cached reference trajectory", coarse_npy)
+    else:
+        t = time.time()
+        snaps, its, rel = run_reference(hn, N, T, (5.19, 0.026))
+        print(f"coarse250: reference run {time.time() - t:.0f}s")
+    out = _summaries(np.asarray(snaps), N, (1, 2, 100, 500))
+    out["its"], out["rel"] = its, rel
+    np.savez_compressed(os.path.join(HERE, "ref_coarse250.npz"), **out)
+
+
+def make_fine750(hn):
+    N, T = 750, 2
+    t = time.time()
+    snaps, its, rel = run_reference(hn, N, T, (5.19, 0.026))
+    print(f"fine750: {time.time() - t:.0f}s its={its} rel={rel}")
+    out = _summaries(snaps, N, ())
+    out["its"], out["rel"] = its, rel
+    mid = N // 2
+    out["u_row_all"] = snaps[:N * N].reshape(N, N, -1)[mid, :, :].T.copy()
+    out["v_col_all"] = snaps[N * N:].reshape(N, N, -1)[:, mid, :].T.copy()
+    np.savez_compressed(os.path.join(HERE, "ref_fine750.npz"), **out)
+
+
+def scan_pickle(path, N):
+    """HDM slices from the author's pickled Figure, by scanning byte payloads
+    with pickletools.genops (nothing is unpickled or executed)."""
+    data = open(path, "rb").read()
+    arrs = []
+    for op, arg, _pos in pickletools.genops(io.BytesIO(data)):
+        if op.name in ("SHORT_BINBYTES", "BINBYTES", "BINBYTES8") and len(arg) == 8 * N:
+            arrs.append(np.frombuffer(arg, dtype="<f8").copy())
+    g = np.linspace(0, 100, N + 1)
+    xc = (g[1:] + g[:-1]) / 2
+    ys = [a for a in arrs if not np.array_equal(a, xc)]
+    # each line is stored twice (_xorig/_x paths): keep one of each pair
+    ys = ys[::2]
+    assert len(ys) == 24, len(ys)
+    # order: axis-1 (row N//2) HDM x6, HPROM x6; axis-2 (column N//2) HDM x6, HPROM x6
+    return np.stack(ys[0:6]), np.stack(ys[12:18])
+
+
+def make_pickles():
+    out = {}
+    for tag, d, N in (("coarse", COARSE, 250), ("fine", FINE, 750)):
+        row, col = scan_pickle(os.path.join(d, "predict_mu_5.19e+00_2.60e-02_hprom.pickle"), N)
+        out[f"{tag}_u_row"] = row
+        out[f"{tag}_u_col"] = col
+        out[f"{tag}_steps"] = np.arange(0, 501, 100)
+    np.savez_compressed(os.path.join(HERE, "author_pickles.npz"), **out)
+    print("pickles done")
+
+
+def make_logs():
+    out = {}
+    for name in ("output_55034725.log", "output_54767262.log"):
+        text = open(os.path.join(FINE, name)).read()
+        runs, cur, mu = [], None, None
+        for line in text.splitlines():
+            m = re.match(r"^Running HDM for mu1=([0-9.]+)", line)
+            if m:
+                cur = {"mu1": float(m.group(1)), "its": [], "rel": []}
+                runs.append(cur)
+                continue
+            m = NEWTON_RE.match(line.strip())
+            if m and cur is not None and len(cur["its"]) < 500:
+                cur["its"].append(int(m.group(1)))
+                cur["rel"].append(float(m.group(2)))
+            m = re.match(r"^Elapsed time: ([0-9.e+]+)", line)
+            if m and cur is not None and "elapsed_s" not in cur:
+                cur["elapsed_s"] = float(m.group(1))
+        out[name] = runs
+    with open(os.path.join(HERE, "author_logs.json"), "w") as f:
+        json.dump(out, f)
+    print("logs done")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-750", action="store_true")
+    ap.add_argument("--coarse-npy", default="/tmp/oracle_probe/hdm_snaps_mu1_5.19_mu2_0.026.npy")
+    ap.add_argument("--coarse-log", default="/tmp/oracle_probe/coarse_full.log")
+    ap.add_argument("--only", default="")
+    args = ap.parse_args()
+    only = set(args.only.split(",")) if args.only else None
+    make_pickles() if not only or "pickles" in only else None
+    make_logs() if not only or "logs" in only else None
+    scratch = tempfile.mkdtemp(prefix="golden_")
+    cwd = os.getcwd()
+    os.chdir(scratch)
+    try:
+        hn = _import_reference()
+        if not only or "small" in only:
+            make_small(hn)
+        if not only or "ops" in only:
+            make_ops(hn)
+        if not only or "coarse" in only:
+            make_coarse250(hn, args.coarse_npy, args.coarse_log)
+        if (not only or "fine" in only) and not args.skip_750:
+            make_fine750(hn)
+    finally:
+        os.chdir(cwd)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,195 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle and the
+reference's golden vectors.  Bars: bitwise for equal op order and tiling,
+rel-L2 <= 1e-10 against the reference trajectory (north-star tolerance).
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+TOL4ULP = 2.0 ** -50
+REF_TOL = 1e-10  # BASELINE.json north star: snapshots within 1e-10 rel-L2
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(b))
+
+
+def make_ctx(N, mu=(5.19, 0.026), dt=0.05, ny=None, **opts):
+    from finitedifference_amd.solver import FOMContext
+    ny = N if ny is None else ny
+    ctx = FOMContext(N, ny, **opts)
+    gx = np.linspace(0, 100, N + 1)
+    gy = np.linspace(0, 100, ny + 1)
+    ctx.set_problem(gx, gy, dt, mu, allow_nonsquare=(ny != N))
+    return ctx
+
+
+def state_after(orc, P, steps):
+    w = np.ones(P.m)
+    for _ in range(steps):
+        w = P.march_step(w)
+    return w
+
+
+# ---------------------------------------------------------------- K1 / K2 --
+@pytest.mark.parametrize("N", [16, 64, 250])
+def test_residual_bitwise_vs_oracle_and_reference(gpu, orc, N):
+    g = golden("ref_ops.npz")
+    mu = tuple(g[f"n{N}_mu"])
+    w, wp = g[f"n{N}_w"], g[f"n{N}_wp"]
+    ctx = make_ctx(N, mu)
+    r, nrm = ctx.residual(w, wp)
+    P = orc.Problem(N, mu=mu)
+    ro = P.residual(w, wp)
+    assert np.array_equal(r, ro), "GPU residual must equal the oracle bit for bit"
+    assert abs(nrm - np.linalg.norm(ro)) <= 1e-13 * np.linalg.norm(ro)
+    if N <= 64:
+        assert rel(r, g[f"n{N}_res"]) <= 1e-15
+    else:
+        assert np.allclose(r[g["n250_res_idx"]], g["n250_res_at"], rtol=1e-14, atol=0)
+
+
+@pytest.mark.parametrize("N", [16, 64, 250])
+def test_jvp_bitwise_vs_oracle_and_reference(gpu, orc, N):
+    g = golden("ref_ops.npz")
+    w, x = g[f"n{N}_w"], g[f"n{N}_x"]
+    ctx = make_ctx(N, tuple(g[f"n{N}_mu"]))
+    y = ctx.jvp(w, x)
+    P = orc.Problem(N, mu=tuple(g[f"n{N}_mu"]))
+    assert np.array_equal(y, P.jvp(w, x))
+    if N <= 64:
+        assert rel(y, g[f"n{N}_jx"]) <= 1e-14
+    else:
+        assert np.allclose(y[g["n250_res_idx"]], g["n250_jx_at"], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("N", [16, 64])
+def test_block_solve_matches_spsolve(gpu, orc, N):
+    g = golden("ref_ops.npz")
+    w, r = g[f"n{N}_w"], g[f"n{N}_res"]
+    ctx = make_ctx(N, tuple(g[f"n{N}_mu"]), tol=0.0)
+    d = ctx.block_solve(w, r)
+    P = orc.Problem(N, mu=tuple(g[f"n{N}_mu"]))
+    assert np.array_equal(d, P.block_solve(w, r)), "tol=0 reaches the sequential fixed point"
+    assert rel(d, g[f"n{N}_solve"]) <= 1e-13  # SuperLU spsolve (C/hypernet2D.py:1854)
+
+
+# ------------------------------------------------------------------ march --
+@pytest.mark.parametrize("N,tw", [(13, 64), (64, 64), (100, 64), (250, 64), (250, 128),
+                                  (300, 128)])
+def test_march_step_bitwise_sequential(gpu, orc, N, tw):
+    """tol = 0: the tile engine's fixed point is the sequential march."""
+    P = orc.Problem(N)
+    wp = state_after(orc, P, 7)
+    ctx = make_ctx(N, tile_w=tw, tol=0.0)
+    snaps, st, its, _ = ctx.run(wp, 1)
+    assert st["unconverged_steps"] == 0
+    assert np.array_equal(snaps[:, 1], P.march_step(wp))
+
+
+@pytest.mark.parametrize("N,tw", [(250, 64), (333, 64), (512, 128)])
+def test_march_step_bitwise_tiled_schedule(gpu, orc, N, tw):
+    """tol = 4 ulp: the GPU reproduces the CPU schedule simulator bit for bit,
+    and both sit within ~1e-16 of the sequential march."""
+    P = orc.Problem(N)
+    wp = state_after(orc, P, 20)
+    ctx = make_ctx(N, tile_w=tw, tol=TOL4ULP)
+    snaps, st, its, _ = ctx.run(wp, 1)
+    ws, k, _ = P.march_tiled(wp, tw=tw, tol=TOL4ULP)
+    assert np.array_equal(snaps[:, 1], ws)
+    assert its[0] == k
+    assert rel(ws, P.march_step(wp)) <= 1e-14
+
+
+def test_march_solves_the_reference_residual(gpu):
+    """Size-independent property at the bench size: R(w_next; w) ~ 0."""
+    N = 1024
+    ctx = make_ctx(N)
+    w0 = np.ones(2 * N * N)
+    snaps, st, its, _ = ctx.run(w0, 3)
+    r0, n0 = ctx.residual(snaps[:, 2], snaps[:, 2])
+    r1, n1 = ctx.residual(snaps[:, 3], snaps[:, 2])
+    assert n1 / n0 < 1e-13
+    assert st["unconverged_steps"] == 0
+
+
+# ------------------------------------------------------ full trajectories --
+@pytest.mark.parametrize("tag", ["n8", "n13", "n16", "n16b", "n50", "n100"])
+def test_small_trajectories_vs_reference(gpu, tag):
+    g = golden("ref_small.npz")
+    N, T, mu1, mu2, dt = g[f"{tag}_meta"]
+    N, T = int(N), int(T)
+    ctx = make_ctx(N, (mu1, mu2), dt)
+    snaps, st, its, _ = ctx.run(np.ones(2 * N * N), T)
+    ref = g[f"{tag}_snaps"]
+    assert snaps.shape == ref.shape and snaps.flags.c_contiguous
+    worst = max(rel(snaps[:, j], ref[:, j]) for j in range(1, T + 1))
+    assert worst <= REF_TOL, worst
+
+
+@pytest.mark.parametrize("tag", ["n8", "n13", "n16b", "n50"])
+def test_newton_mode_counts_match_reference(gpu, tag):
+    """solver='newton' is the reference algorithm: same Newton update counts
+    per step as the reference's printed log."""
+    g = golden("ref_small.npz")
+    N, T, mu1, mu2, dt = g[f"{tag}_meta"]
+    N, T = int(N), min(int(T), 60)
+    ctx = make_ctx(N, (mu1, mu2), dt)
+    snaps, st, its, rl = ctx.run(np.ones(2 * N * N), T, solver="newton")
+    assert np.array_equal(its, g[f"{tag}_its"][:T])
+    ref = g[f"{tag}_snaps"][:, :T + 1]
+    assert max(rel(snaps[:, j], ref[:, j]) for j in range(1, T + 1)) <= 1e-13
+
+
+def test_coarse250_full_run_vs_reference(gpu, orc):
+    """C/run_fom.py defaults: 250^2, 500 steps, mu=(5.19, 0.026)."""
+    g = golden("ref_coarse250.npz")
+    N, T = 250, 500
+    ctx = make_ctx(N)
+    snaps, st, its, _ = ctx.run(np.ones(2 * N * N), T)
+    assert st["unconverged_steps"] == 0
+    for j in (1, 2, 100, 500):
+        assert rel(snaps[:, j], g[f"state_{j}"]) <= REF_TOL
+    norms = np.sqrt(np.square(snaps).sum(axis=0))
+    assert np.allclose(norms, g["col_norm"], rtol=1e-12, atol=0)
+    n = N * N
+    U = snaps[:n].reshape(N, N, -1)
+    steps = g["slice_steps"]
+    assert rel(U[N // 2, :, steps].T, g["u_row"].T) <= REF_TOL
+    ws = orc.Problem(N).fom(np.ones(2 * n), T)[0]
+    assert max(rel(snaps[:, j], ws[j]) for j in range(1, T + 1, 7)) <= 1e-13
+
+
+def test_fine750_vs_author_pickle(gpu):
+    """F/ grid, 500 steps: the author's pickled HDM mid-line slices."""
+    g = golden("author_pickles.npz")
+    N, T = 750, 500
+    ctx = make_ctx(N)
+    snaps, st, its, _ = ctx.run(np.ones(2 * N * N), T, snap_every=100)
+    n = N * N
+    U = snaps[:n].reshape(N, N, -1)
+    for k in range(6):
+        assert rel(U[N // 2, :, k], g["fine_u_row"][k]) <= REF_TOL
+        assert rel(U[:, N // 2, k], g["fine_u_col"][k]) <= REF_TOL
+
+
+def test_snap_every_layout(gpu):
+    N, T = 64, 12
+    ctx = make_ctx(N)
+    full, _, _, _ = ctx.run(np.ones(2 * N * N), T)
+    sub, _, _, _ = ctx.run(np.ones(2 * N * N), T, snap_every=4)
+    assert sub.shape == (2 * N * N, 4)
+    assert np.array_equal(sub, full[:, ::4])
+
+
+def test_device_resident_advance_matches_run(gpu):
+    N, T = 128, 9
+    ctx = make_ctx(N)
+    full, _, _, _ = ctx.run(np.ones(2 * N * N), T)
+    ctx.upload(np.ones(2 * N * N))
+    st = ctx.advance(T)
+    assert st["steps"] == T
+    assert np.array_equal(ctx.download(), full[:, T])

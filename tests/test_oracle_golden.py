@@ -1,0 +1,184 @@
+"""Pin the CPU oracle to the reference (CPU only, no GPU).
+
+The oracle (oracle/burgers_oracle.c) is the checker of every GPU parity test,
+so it is checked here against every golden vector the reference provides:
+fixtures made by importing the Python reference (tests/golden/make_golden.py),
+the author's pickled HDM slices and the author's SLURM Newton logs.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden
+
+
+def rel(a, b):
+    return float(np.linalg.norm(np.asarray(a) - np.asarray(b)) / np.linalg.norm(b))
+
+
+# ---------------------------------------------------------- single calls ---
+@pytest.mark.parametrize("N", [16, 64, 250])
+def test_residual_vs_reference(orc, N):
+    g = golden("ref_ops.npz")
+    P = orc.Problem(N, mu=tuple(g[f"n{N}_mu"]))
+    r = P.residual(g[f"n{N}_w"], g[f"n{N}_wp"])
+    if N <= 64:
+        assert rel(r, g[f"n{N}_res"]) <= 1e-15
+        # res2D (1-D operator form, C/hypernet2D.py:2468) is the same residual
+        assert rel(r, g[f"n{N}_res1d"]) <= 1e-15
+    else:
+        assert np.allclose(r[g["n250_res_idx"]], g["n250_res_at"], rtol=1e-14, atol=0)
+        assert abs(np.linalg.norm(r) - g["n250_res_norm"]) <= 1e-13 * g["n250_res_norm"]
+
+
+@pytest.mark.parametrize("N", [16, 64, 250])
+def test_jvp_vs_reference(orc, N):
+    g = golden("ref_ops.npz")
+    P = orc.Problem(N, mu=tuple(g[f"n{N}_mu"]))
+    y = P.jvp(g[f"n{N}_w"], g[f"n{N}_x"])
+    if N <= 64:
+        assert rel(y, g[f"n{N}_jx"]) <= 1e-14
+    else:
+        assert abs(np.linalg.norm(y) - g["n250_jx_norm"]) <= 1e-13 * g["n250_jx_norm"]
+
+
+@pytest.mark.parametrize("N", [16, 64])
+def test_block_solve_vs_spsolve(orc, N):
+    g = golden("ref_ops.npz")
+    P = orc.Problem(N, mu=tuple(g[f"n{N}_mu"]))
+    d = P.block_solve(g[f"n{N}_w"], g[f"n{N}_res"])
+    assert rel(d, g[f"n{N}_solve"]) <= 1e-13
+    # and it is the inverse of the Jacobian action
+    assert rel(P.jvp(g[f"n{N}_w"], d), g[f"n{N}_res"]) <= 1e-13
+
+
+# ------------------------------------------------------ trajectories -------
+@pytest.mark.parametrize("tag", ["n8", "n13", "n16", "n16b", "n50", "n100"])
+def test_newton_fom_reproduces_reference(orc, tag):
+    g = golden("ref_small.npz")
+    N, T, mu1, mu2, dt = g[f"{tag}_meta"]
+    N, T = int(N), int(T)
+    P = orc.Problem(N, dt=dt, mu=(mu1, mu2))
+    snaps, its, rl = P.fom(np.ones(2 * N * N), T, solver="newton")
+    ref = g[f"{tag}_snaps"]
+    assert np.array_equal(its, g[f"{tag}_its"])
+    assert max(rel(snaps[j], ref[:, j]) for j in range(1, T + 1)) <= 1e-13
+
+
+@pytest.mark.parametrize("tag", ["n8", "n13", "n16", "n16b", "n50", "n100"])
+def test_march_fom_matches_reference(orc, tag):
+    g = golden("ref_small.npz")
+    N, T, mu1, mu2, dt = g[f"{tag}_meta"]
+    N, T = int(N), int(T)
+    P = orc.Problem(N, dt=dt, mu=(mu1, mu2))
+    snaps, _, _ = P.fom(np.ones(2 * N * N), T, solver="march")
+    ref = g[f"{tag}_snaps"]
+    assert max(rel(snaps[j], ref[:, j]) for j in range(1, T + 1)) <= 1e-12
+
+
+def test_coarse250_reference_run(orc):
+    """C/run_fom.py defaults, all 500 steps, against the reference run."""
+    g = golden("ref_coarse250.npz")
+    N, T = 250, 500
+    P = orc.Problem(N)
+    snaps, _, _ = P.fom(np.ones(2 * N * N), T, solver="march")
+    for j in (1, 2, 100, 500):
+        assert rel(snaps[j], g[f"state_{j}"]) <= 1e-12
+    assert np.allclose(np.sqrt(np.square(snaps).sum(axis=1)), g["col_norm"], rtol=1e-12, atol=0)
+    assert np.allclose(snaps.sum(axis=1), g["col_sum"], rtol=1e-12, atol=0)
+    n = N * N
+    steps = g["slice_steps"]
+    U = snaps[steps, :n].reshape(len(steps), N, N)
+    V = snaps[steps, n:].reshape(len(steps), N, N)
+    assert rel(U[:, N // 2, :], g["u_row"]) <= 1e-12
+    assert rel(U[:, :, N // 2], g["u_col"]) <= 1e-12
+    assert rel(V[:, N // 2, :], g["v_row"]) <= 1e-12
+    assert rel(V[:, :, N // 2], g["v_col"]) <= 1e-12
+
+
+def test_coarse250_newton_counts_vs_reference_log(orc):
+    """Per-step Newton update counts of the reference's 250^2 run."""
+    g = golden("ref_coarse250.npz")
+    N, T = 250, 60
+    P = orc.Problem(N)
+    _, its, rl = P.fom(np.ones(2 * N * N), T, solver="newton")
+    assert np.array_equal(its, g["its"][:T])
+    # printed relative residuals agree to the printed precision (3 digits)
+    assert np.allclose(rl, g["rel"][:T], rtol=1e-2, atol=0)
+
+
+def test_author_pickle_coarse(orc):
+    """The author's own pickled HDM slices (C/predict_mu_5.19e+00_2.60e-02_hprom.pickle)."""
+    g = golden("author_pickles.npz")
+    N, T = 250, 500
+    P = orc.Problem(N)
+    snaps, _, _ = P.fom(np.ones(2 * N * N), T, solver="march")
+    n = N * N
+    for k, j in enumerate(g["coarse_steps"]):
+        u = snaps[j, :n].reshape(N, N)
+        assert rel(u[N // 2, :], g["coarse_u_row"][k]) <= 1e-12
+        assert rel(u[:, N // 2], g["coarse_u_col"][k]) <= 1e-12
+
+
+@pytest.mark.slow
+def test_author_pickle_fine750(orc):
+    """F/ grid (750^2), 500 steps, against the author's pickled slices."""
+    g = golden("author_pickles.npz")
+    N = 750
+    P = orc.Problem(N)
+    w = np.ones(2 * N * N)
+    n = N * N
+    for step in range(501):
+        if step % 100 == 0:
+            k = step // 100
+            u = w[:n].reshape(N, N)
+            assert rel(u[N // 2, :], g["fine_u_row"][k]) <= 1e-12
+            assert rel(u[:, N // 2], g["fine_u_col"][k]) <= 1e-12
+        if step < 500:
+            w = P.march_step(w)
+
+
+def test_fine750_first_steps_and_author_log(orc):
+    """750^2: reference run (2 steps) and the author's SLURM log
+    F/output_55034725.log (Newton counts 5, 4, ... ; printed residuals)."""
+    g = golden("ref_fine750.npz")
+    logs = json.load(open(os.path.join(GOLDEN, "author_logs.json")))
+    run = logs["output_55034725.log"][0]
+    assert run["mu1"] == 5.19
+    N = 750
+    P = orc.Problem(N)
+    w = np.ones(2 * N * N)
+    w1, its1, rel1 = P.newton_step(w)
+    w2, its2, rel2 = P.newton_step(w1)
+    assert [its1, its2] == list(g["its"]) == run["its"][:2]
+    assert f"{rel1:3.2e}" == f"{run['rel'][0]:3.2e}"  # "5.82e-16" in the author's log
+    n = N * N
+    assert rel(w2[:n].reshape(N, N)[N // 2, :], g["u_row_all"][2]) <= 1e-13
+    assert rel(w2[n:].reshape(N, N)[:, N // 2], g["v_col_all"][2]) <= 1e-13
+    m1 = P.march_step(w)
+    assert rel(m1, w1) <= 1e-13
+    assert np.all(np.asarray(run["its"][1:]) == 4)
+
+
+# ------------------------------------------------- tile schedule (engine) --
+@pytest.mark.parametrize("N,tw", [(13, 64), (130, 64), (250, 128)])
+def test_tile_schedule_bitwise_at_tol0(orc, N, tw):
+    P = orc.Problem(N)
+    w = np.ones(2 * N * N)
+    for _ in range(5):
+        w = P.march_step(w)
+    ws, k, done = P.march_tiled(w, tw=tw, tol=0.0)
+    assert np.array_equal(ws, P.march_step(w))
+
+
+def test_tile_schedule_converges_in_few_passes(orc):
+    N = 512
+    P = orc.Problem(N)
+    w = np.ones(2 * N * N)
+    for _ in range(30):
+        w = P.march_step(w)
+    ws, k, done = P.march_tiled(w, tw=64, tol=2.0 ** -50)
+    assert k <= 6
+    assert rel(ws, P.march_step(w)) <= 1e-15
