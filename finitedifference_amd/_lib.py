@@ -38,16 +38,17 @@ class BurgStats(ctypes.Structure):
         ("unconverged_steps", ctypes.c_int32),
         ("newton_updates", ctypes.c_int64),
         ("newton_max_updates", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("par_passes", ctypes.c_int32),
         ("loop_ms", ctypes.c_double),
         ("flush_ms", ctypes.c_double),
         ("march_kernel_ms", ctypes.c_double),
         ("march_launches", ctypes.c_int64),
         ("last_rel", ctypes.c_double),
+        ("tail_passes", ctypes.c_int64),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class BurgersError(RuntimeError):

@@ -35,7 +35,9 @@ struct Engine {
     double *nb[2];     // [ntiles][2][tw]
     double *wused;     // [ntiles][2][64]
     double *sused;     // [ntiles][2][tw]
-    int *counters;     // [kmax + 2]  tiles marched per pass (index = pass)
+    int *counters;     // [kbound + 2]  tiles marched per pass (index = pass)
+    int *ticket;       // arrival counter of the final pass (reset by its last workgroup)
+    int kbound;        // #tile anti-diagonals + 1: passes that always reach the fixed point
     // Slab halo (multi-GPU): outflow (YH, YG) of the row below this slab,
     // [2][nx], and that row's previous-step state (u, v) [2][nx] for the
     // pass-1 guess.  nullptr => bottom rows see the domain boundary (zero).
@@ -53,6 +55,7 @@ struct DevStats {
     int max_passes;
     int unconverged_steps;
     long long steps;
+    long long tail_passes;  // passes run by the final kernel's last workgroup
 };
 
 }  // namespace burg
@@ -60,11 +63,12 @@ struct DevStats {
 // ---- host-side launch wrappers (defined in the .hip files) ----------------
 namespace burg {
 
+// pass = 1..P (final = false) over all tiles, then pass P+1 with final = true
 int launch_march_pass(const Coeffs &cf, const Engine &eg, const double *wp, double *w,
-                      int pass, hipStream_t st);
+                      int pass, bool final, DevStats *stats, hipStream_t st);
 int launch_solve_pass(const Coeffs &cf, const Engine &eg, const double *w,
-                      const double *rhs, double *delta, int pass, hipStream_t st);
-int launch_pass_epilogue(const Engine &eg, int kmax, DevStats *stats, hipStream_t st);
+                      const double *rhs, double *delta, int pass, bool final,
+                      DevStats *stats, hipStream_t st);
 
 int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
                     double *partials, double *sumsq, const double *halo_w,

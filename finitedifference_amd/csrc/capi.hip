@@ -85,13 +85,13 @@ struct burg_ctx {
     Coeffs cf{};
 
     // engine
-    int tw = 64, max_passes_opt = 0, profile = 0;
+    int tw = 64, par_passes_opt = 0, profile = 0;
     double tol = 0x1p-50;  // 4 ulp relative
     Engine eg{};
-    int kmax = 0;
+    int par_passes = 3;  // parallel passes before the final pass
     double *d_edges = nullptr;
     int *d_counters = nullptr;
-    DevStats *d_stats = nullptr;
+    DevStats *d_stats = nullptr, *d_stats_solve = nullptr;
 
     // states (ping-pong) and scratch
     double *d_state[2] = {nullptr, nullptr};
@@ -137,9 +137,11 @@ int engine_alloc(burg_ctx *c)
     c->eg.halo_flux = nullptr;
     c->eg.halo_wp = nullptr;
     const int bound = nti + ntj;  // #anti-diagonals + 1 passes always reach the fixed point
-    c->kmax = c->max_passes_opt > 0 ? std::min(c->max_passes_opt, bound) : bound;
-    if (int e = dalloc(&c->d_counters, (size_t)c->kmax + 2)) return e;
-    HIPCHK(hipMemsetAsync(c->d_counters, 0, sizeof(int) * (c->kmax + 2), c->stream));
+    c->eg.kbound = bound;
+    c->par_passes = c->par_passes_opt > 0 ? std::min(c->par_passes_opt, bound - 1) : std::min(3, bound - 1);
+    if (int e = dalloc(&c->d_counters, (size_t)bound + 3)) return e;
+    HIPCHK(hipMemsetAsync(c->d_counters, 0, sizeof(int) * (bound + 3), c->stream));
+    c->eg.ticket = c->d_counters + bound + 2;
     c->eg.counters = c->d_counters;
     return 0;
 }
@@ -164,33 +166,36 @@ int check_ready(burg_ctx *c)
     return 0;
 }
 
-// One implicit step wp -> w by the march engine (all passes + epilogue).
+// One implicit step wp -> w by the march engine: P parallel passes + final.
 int march_step(burg_ctx *c, const double *wp, double *w)
 {
-    for (int k = 1; k <= c->kmax; ++k) {
+    const int P = c->par_passes;
+    for (int k = 1; k <= P + 1; ++k) {
+        hipEvent_t a = nullptr, b = nullptr;
         if (c->profile) {
-            hipEvent_t a, b;
             HIPCHK(hipEventCreate(&a));
             HIPCHK(hipEventCreate(&b));
             HIPCHK(hipEventRecord(a, c->stream));
-            CHK(launch_march_pass(c->cf, c->eg, wp, w, k, c->stream));
+        }
+        CHK(launch_march_pass(c->cf, c->eg, wp, w, k, k == P + 1, c->d_stats, c->stream));
+        if (c->profile) {
             HIPCHK(hipEventRecord(b, c->stream));
             c->prof_ev.push_back(a);
             c->prof_ev.push_back(b);
-        } else {
-            CHK(launch_march_pass(c->cf, c->eg, wp, w, k, c->stream));
         }
     }
-    CHK(launch_pass_epilogue(c->eg, c->kmax, c->d_stats, c->stream));
     return 0;
 }
 
 // Exact linear solve J(w) delta = rhs with the SOLVE cell.
 int block_solve(burg_ctx *c, const double *w, const double *rhs, double *delta)
 {
-    for (int k = 1; k <= c->kmax; ++k)
-        CHK(launch_solve_pass(c->cf, c->eg, w, rhs, delta, k, c->stream));
-    CHK(launch_pass_epilogue(c->eg, c->kmax, c->d_stats, c->stream));
+    if (c->tw != 64)
+        return fail(BURG_EINVAL, "the exact block solve (newton solver) needs tile_w = 64");
+    const int P = c->par_passes;
+    for (int k = 1; k <= P + 1; ++k)
+        CHK(launch_solve_pass(c->cf, c->eg, w, rhs, delta, k, k == P + 1, c->d_stats_solve,
+                              c->stream));
     return 0;
 }
 
@@ -258,6 +263,8 @@ int read_stats(burg_ctx *c, burg_stats *st)
         st->passes = ds.passes;
         st->max_passes = ds.max_passes;
         st->unconverged_steps = ds.unconverged_steps;
+        st->tail_passes = ds.tail_passes;
+        st->par_passes = c->par_passes;
     }
     return 0;
 }
@@ -312,11 +319,12 @@ int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, 
         return fail(BURG_EHIP, "stream/event creation failed");
     }
     if ((e = dalloc(&c->d_state[0], c->m())) || (e = dalloc(&c->d_state[1], c->m())) ||
-        (e = dalloc(&c->d_stats, 1))) {
+        (e = dalloc(&c->d_stats, 1)) || (e = dalloc(&c->d_stats_solve, 1))) {
         burg_ctx_destroy(c);
         return e;
     }
     (void)hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream);
+    (void)hipMemsetAsync(c->d_stats_solve, 0, sizeof(DevStats), c->stream);
     if ((e = engine_alloc(c))) {
         burg_ctx_destroy(c);
         return e;
@@ -338,6 +346,7 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_edges);
     dfree(c->d_counters);
     dfree(c->d_stats);
+    dfree(c->d_stats_solve);
     dfree(c->d_state[0]);
     dfree(c->d_state[1]);
     dfree(c->d_r);
@@ -385,7 +394,7 @@ int burg_set_problem(burg_ctx *c, const double *inv_dx, const double *inv_dy,
     return BURG_OK;
 }
 
-int burg_set_options(burg_ctx *c, int tile_w, int max_passes, double tol, int profile)
+int burg_set_options(burg_ctx *c, int tile_w, int par_passes, double tol, int profile)
 {
     if (!c) return fail(BURG_EINVAL, "null context");
     if (tile_w != 64 && tile_w != 128) return fail(BURG_EINVAL, "tile_w must be 64 or 128");
@@ -393,7 +402,7 @@ int burg_set_options(burg_ctx *c, int tile_w, int max_passes, double tol, int pr
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->tw = tile_w;
-    c->max_passes_opt = max_passes;
+    c->par_passes_opt = par_passes;
     c->tol = tol;
     c->profile = profile ? 1 : 0;
     return engine_alloc(c);

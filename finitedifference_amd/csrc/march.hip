@@ -15,10 +15,18 @@
 // Op order of both cells is normative: oracle/burgers_oracle.c restates it
 // (orc_march_step / orc_block_solve / orc_march_tiled_sim) and the GPU result
 // is compared against it (bitwise for equal tiling and tolerance).
+//
+// Schedule per step: passes 1..P are launched over all tiles (one wavefront
+// per tile, block Jacobi between tiles); pass P+1 is the FINAL kernel: every
+// tile checks its inflow, and the last workgroup to finish (arrival ticket,
+// agent-scope release/acquire) runs any further passes itself until no tile
+// moves -- so a step always ends at the fixed point, with no host round trip
+// and no idle launches.  It also folds the step's statistics.
 #include "burg_internal.h"
 
 namespace burg {
 namespace {
+
 
 __device__ __forceinline__ double shr1(double x)
 {
@@ -42,74 +50,168 @@ __device__ __forceinline__ bool moved(double a, double b, double tol)
 }
 
 // ---------------------------------------------------------------------------
-// MARCH cell: inputs wp (up, vp); outputs w (u, v).
+// MARCH cell: inputs wp = (up, vp); outputs w = (u, v).
 // Outflows: east (XF, XH) = ax*(F+Fp), ax*(H+Hp); north (YH, YG) = ay*(H+Hp),
 // ay*(G+Gp), with F = u^2/2, G = v^2/2, H = u*v/2 (C/hypernet2D.py:2544-2547).
 struct MarchCell {
-    struct In {
-        const double *p0;  // up plane (wp)
-        const double *p1;  // vp plane
-        double *o0;        // u plane (w)
-        double *o1;        // v plane
+    static constexpr int NIN = 2;
+    struct Io {
+        const double *in[NIN];  // up, vp planes
+        double *out[2];         // u, v planes
     };
-    struct Pre {
-        double xfp, xhp, yhp, ygp, bu, bv;
+    struct Row {
+        double ay, hy, lb;
     };
-    __device__ static Pre pre(const Coeffs &cf, double ax, double ay, double sl, double pu,
-                              double pv)
+    __device__ static Row row(const Coeffs &cf, int r)
     {
-        Pre p;
-        const double hu = 0.5 * pu;
-        p.xfp = ax * (hu * pu);
-        p.xhp = ax * (hu * pv);
-        p.yhp = ay * (hu * pv);
-        p.ygp = ay * ((0.5 * pv) * pv);
-        p.bu = ((pu - p.xfp) - p.yhp) + sl;
-        p.bv = (pv - p.ygp) - p.xhp;
-        return p;
+        Row w;
+        w.ay = cf.alpha * cf.inv_dy[r];
+        w.hy = 0.5 * w.ay;
+        w.lb = cf.lbc[r];
+        return w;
     }
-    // solve one cell given west (xf, xh) and south (yh, yg) inflow; returns
-    // state and overwrites the inflow registers with this cell's outflow.
-    __device__ static void step(const Pre &p, double hx, double hy, double &xf, double &xh,
-                                double &yh, double &yg, double &nu, double &nv)
+    // solve cell (r, c) given west (e0=XF, e1=XH) and south (n0=YH, n1=YG)
+    // inflow; the inflow registers are overwritten with this cell's outflow.
+    __device__ static void cell(const Coeffs &cf, const Row &rw, const double (&x)[NIN],
+                                double invdx, double srcc, int c, double &e0, double &e1,
+                                double &n0, double &n1, double &o0, double &o1)
     {
-        const double cu = (p.bu + xf) + yh;
-        const double cv = (p.bv + yg) + xh;
-        const double mm = fma(hx, cu, hy * cv);
+        const double pu = x[0], pv = x[1];
+        const double ax = cf.alpha * invdx;
+        const double hx = 0.5 * ax;
+        const double sl = c == 0 ? srcc + rw.lb : srcc;
+        const double hu = 0.5 * pu;
+        const double xfp = ax * (hu * pu);
+        const double xhp = ax * (hu * pv);
+        const double yhp = rw.ay * (hu * pv);
+        const double ygp = rw.ay * ((0.5 * pv) * pv);
+        const double bu = ((pu - xfp) - yhp) + sl;
+        const double bv = (pv - ygp) - xhp;
+        const double cu = (bu + e0) + n0;
+        const double cv = (bv + n1) + e1;
+        const double mm = fma(hx, cu, rw.hy * cv);
         const double s = 0.5 + sqrt(0.25 + mm);
         const double rs = 1.0 / s;
-        nu = cu * rs;
-        nv = cv * rs;
+        const double nu = cu * rs, nv = cv * rs;
         const double hxu = hx * nu;
-        xf = fma(hxu, nu, p.xfp);
-        xh = fma(hxu, nv, p.xhp);
-        yh = fma(hy * nu, nv, p.yhp);
-        yg = fma(hy * nv, nv, p.ygp);
+        e0 = fma(hxu, nu, xfp);
+        e1 = fma(hxu, nv, xhp);
+        n0 = fma(rw.hy * nu, nv, yhp);
+        n1 = fma(rw.hy * nv, nv, ygp);
+        o0 = nu;
+        o1 = nv;
     }
-    // pass-1 guess of a neighbour's outflow: "the neighbour did not move"
-    __device__ static void guess_e(double ax, double hx, double pu, double pv, double &xf,
-                                   double &xh)
+    // pass-1 guesses of a neighbour's outflow: "the neighbour did not move"
+    __device__ static void guess_e(const Coeffs &cf, const Io &io, int r, int c, double &e0,
+                                   double &e1)
     {
+        const size_t i = (size_t)r * cf.nx + c;
+        const double pu = io.in[0][i], pv = io.in[1][i];
+        const double ax = cf.alpha * cf.inv_dx[c], hx = 0.5 * ax;
         const double hu = 0.5 * pu;
-        xf = fma(hx * pu, pu, ax * (hu * pu));
-        xh = fma(hx * pu, pv, ax * (hu * pv));
+        e0 = fma(hx * pu, pu, ax * (hu * pu));
+        e1 = fma(hx * pu, pv, ax * (hu * pv));
     }
-    __device__ static void guess_n(double ay, double hy, double pu, double pv, double &yh,
-                                   double &yg)
+    __device__ static void guess_n_vals(double ay, double pu, double pv, double &n0, double &n1)
     {
-        const double hu = 0.5 * pu;
-        yh = fma(hy * pu, pv, ay * (hu * pv));
-        yg = fma(hy * pv, pv, ay * ((0.5 * pv) * pv));
+        const double hy = 0.5 * ay, hu = 0.5 * pu;
+        n0 = fma(hy * pu, pv, ay * (hu * pv));
+        n1 = fma(hy * pv, pv, ay * ((0.5 * pv) * pv));
+    }
+    __device__ static void guess_n(const Coeffs &cf, const Io &io, int r, int c, double &n0,
+                                   double &n1)
+    {
+        const size_t i = (size_t)r * cf.nx + c;
+        guess_n_vals(cf.alpha * cf.inv_dy[r], io.in[0][i], io.in[1][i], n0, n1);
+    }
+    __device__ static void guess_halo(const Coeffs &cf, const Engine &eg, int c, double &n0,
+                                      double &n1)
+    {
+        guess_n_vals(cf.alpha * cf.inv_dy[-1], eg.halo_wp[c], eg.halo_wp[cf.nx + c], n0, n1);
     }
 };
 
-template <int TW>
-__global__ __launch_bounds__(64) void march_pass_kernel(Coeffs cf, Engine eg,
-                                                        MarchCell::In io, int pass)
+// ---------------------------------------------------------------------------
+// SOLVE cell: exact J(w) delta = rhs, J from exact_jac2D (C/hypernet2D.py:2627).
+// Inputs (u, v, ru, rv); outputs (du, dv).  Linearised outflows: east
+// a = ax*u*du, b = 0.5*ax*(v*du + u*dv); north c = 0.5*ay*(v*du + u*dv),
+// d = ay*v*dv.  Same op order as orc_block_solve.  Pass-1 guess: zero.
+struct SolveCell {
+    static constexpr int NIN = 4;
+    struct Io {
+        const double *in[NIN];  // u, v, ru, rv planes
+        double *out[2];         // du, dv planes
+    };
+    struct Row {
+        double ay;
+    };
+    __device__ static Row row(const Coeffs &cf, int r) { return Row{cf.alpha * cf.inv_dy[r]}; }
+    __device__ static void cell(const Coeffs &cf, const Row &rw, const double (&x)[NIN],
+                                double invdx, double, int, double &e0, double &e1, double &n0,
+                                double &n1, double &o0, double &o1)
+    {
+        const double u = x[0], v = x[1];
+        const double ax = cf.alpha * invdx, ay = rw.ay;
+        const double eu = (x[2] + e0) + n0;
+        const double ev = (x[3] + e1) + n1;
+        const double a00 = (1.0 + ax * u) + (0.5 * ay) * v;
+        const double a01 = (0.5 * ay) * u;
+        const double a10 = (0.5 * ax) * v;
+        const double a11 = (1.0 + ay * v) + (0.5 * ax) * u;
+        const double det = a00 * a11 - a01 * a10;
+        const double du = (a11 * eu - a01 * ev) / det;
+        const double dv = (a00 * ev - a10 * eu) / det;
+        const double m = v * du + u * dv;
+        e0 = (ax * u) * du;
+        e1 = (0.5 * ax) * m;
+        n0 = (0.5 * ay) * m;
+        n1 = (ay * v) * dv;
+        o0 = du;
+        o1 = dv;
+    }
+    __device__ static void guess_e(const Coeffs &, const Io &, int, int, double &e0, double &e1)
+    {
+        e0 = e1 = 0.0;
+    }
+    __device__ static void guess_n(const Coeffs &, const Io &, int, int, double &n0, double &n1)
+    {
+        n0 = n1 = 0.0;
+    }
+    __device__ static void guess_halo(const Coeffs &, const Engine &, int, double &n0,
+                                      double &n1)
+    {
+        n0 = n1 = 0.0;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// One tile, one pass, one workgroup of kWaves wavefronts.  Wave 0 gathers the
+// inflow, decides whether the tile must be marched and sweeps it; all waves
+// stage the tile's inputs into LDS with coalesced row loads before the sweep
+// and write the outputs back coalesced after it (the sweeping wave touches
+// only LDS: lane l reads [l][s-l], conflict-free since the pitch TW-1 is odd).
+// Returns true (uniform over the workgroup) if the tile was marched.
+// Generation `cur` of the edge planes receives its outflow (marched or
+// carried), generation `prv` holds the neighbours' outflow of the previous
+// pass.
+constexpr int kWaves = 4;
+constexpr int kThreads = kWaves * kWave;
+
+template <class C, int TW>
+struct TileLds {
+    double x[C::NIN][kWave * TW];  // staged inputs; planes 0/1 are overwritten by outputs
+    double dx[TW], src[TW];        // per-column inv_dx, src of the tile
+    double nout[2][TW];            // north outflow (top row), flushed after the sweep
+    int need;
+};
+
+template <class C, int TW>
+__device__ bool tile_pass(const Coeffs &cf, const Engine &eg, const typename C::Io &io, int t,
+                          int pass, TileLds<C, TW> &sm)
 {
-    const int t = blockIdx.x;
-    if (pass > 1 && eg.counters[pass - 1] == 0) return;  // converged: idempotent pass
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    const int lane = tid & (kWave - 1);
     const int I = t / eg.ntj, J = t - I * eg.ntj;
     const int nx = cf.nx, ny = cf.ny;
     const int r0 = I * kWave, c0 = J * TW;
@@ -117,202 +219,66 @@ __global__ __launch_bounds__(64) void march_pass_kernel(Coeffs cf, Engine eg,
     const bool rowok = lane < nrow;
     const int r = r0 + (rowok ? lane : nrow - 1);
     const int cur = pass & 1, prv = cur ^ 1;
-    constexpr int NQ = TW / kWave;  // S-edge columns held per lane
-    const size_t nplane = (size_t)nx * ny;
-    (void)nplane;
+    constexpr int NQ = TW / kWave;  // south-edge columns held per lane
 
-    // ---- inflow: west (per row) and south (per column, lane l holds l + 64q)
-    double wxf = 0.0, wxh = 0.0;
-    double sh[NQ], sg[NQ];
+    // ---- wave 0: inflow, west (per row) and south (per column, lane l holds l + 64q)
+    double we0 = 0.0, we1 = 0.0;
+    double sn0[NQ], sn1[NQ];
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) sh[q] = sg[q] = 0.0;
-
-    if (J > 0) {
-        if (pass == 1) {
-            const int c = c0 - 1;
-            const size_t i = (size_t)r * nx + c;
-            const double ax = cf.alpha * cf.inv_dx[c];
-            MarchCell::guess_e(ax, 0.5 * ax, io.p0[i], io.p1[i], wxf, wxh);
-        } else {
-            const double *e = eg.eb[prv] + (size_t)(t - 1) * 2 * kWave;
-            wxf = e[lane];
-            wxh = e[kWave + lane];
-        }
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int col = lane + kWave * q;
-        if (col >= ncol) continue;
-        const int c = c0 + col;
-        if (I > 0) {
-            if (pass == 1) {
-                const size_t i = (size_t)(r0 - 1) * nx + c;
-                const double ay = cf.alpha * cf.inv_dy[r0 - 1];
-                MarchCell::guess_n(ay, 0.5 * ay, io.p0[i], io.p1[i], sh[q], sg[q]);
-            } else {
-                const double *nn = eg.nb[prv] + (size_t)(t - eg.ntj) * 2 * TW;
-                sh[q] = nn[col];
-                sg[q] = nn[TW + col];
-            }
-        } else if (eg.halo_flux != nullptr) {
-            if (pass == 1) {
-                const double ay = cf.alpha * cf.inv_dy[-1];  // row below the slab
-                MarchCell::guess_n(ay, 0.5 * ay, eg.halo_wp[c], eg.halo_wp[nx + c], sh[q],
-                                   sg[q]);
-            } else {
-                sh[q] = eg.halo_flux[c];
-                sg[q] = eg.halo_flux[nx + c];
-            }
-        }
-    }
-
-    // ---- skip test: re-march only if some inflow moved since last used
+    for (int q = 0; q < NQ; ++q) sn0[q] = sn1[q] = 0.0;
     double *wu = eg.wused + (size_t)t * 2 * kWave;
     double *su = eg.sused + (size_t)t * 2 * TW;
-    if (pass > 1) {
-        bool mv = rowok && (moved(wxf, wu[lane], eg.tol) || moved(wxh, wu[kWave + lane], eg.tol));
+    if (wave == 0) {
+        if (J > 0) {
+            if (pass == 1) {
+                C::guess_e(cf, io, r, c0 - 1, we0, we1);
+            } else {
+                const double *e = eg.eb[prv] + (size_t)(t - 1) * 2 * kWave;
+                we0 = e[lane];
+                we1 = e[kWave + lane];
+            }
+        }
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
             const int col = lane + kWave * q;
-            if (col < ncol)
-                mv = mv || moved(sh[q], su[col], eg.tol) || moved(sg[q], su[TW + col], eg.tol);
-        }
-        if (!__any(mv)) {
-            // carry this tile's outflow into the current generation
-            const double *ep = eg.eb[prv] + (size_t)t * 2 * kWave;
-            double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
-            ec[lane] = ep[lane];
-            ec[kWave + lane] = ep[kWave + lane];
-            const double *np_ = eg.nb[prv] + (size_t)t * 2 * TW;
-            double *nc = eg.nb[cur] + (size_t)t * 2 * TW;
-#pragma unroll
-            for (int q = 0; q < 2 * NQ; ++q) nc[lane + kWave * q] = np_[lane + kWave * q];
-            return;
-        }
-    }
-    if (rowok) {
-        wu[lane] = wxf;
-        wu[kWave + lane] = wxh;
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int col = lane + kWave * q;
-        if (col < ncol) {
-            su[col] = sh[q];
-            su[TW + col] = sg[q];
-        }
-    }
-
-    // ---- skewed sweep: lane l marches row r0+l, column j = s - l at step s
-    const double ay = cf.alpha * cf.inv_dy[r];
-    const double hy = 0.5 * ay;
-    const double lb = cf.lbc[r];
-    double xf = wxf, xh = wxh;      // running west inflow of my row
-    double yho = 0.0, ygo = 0.0;    // my last north outflow (for lane + 1)
-    double *nout = eg.nb[cur] + (size_t)t * 2 * TW;
-    const int nsteps = ncol + nrow - 1;
-    const size_t rowbase = (size_t)r * nx + c0;
-    for (int s = 0; s < nsteps; ++s) {
-        double yh = shr1(yho), yg = shr1(ygo);
-        if (s < ncol) {  // lane 0 takes the tile's south edge for column s
-            double eh, eg_;
-            if constexpr (NQ == 1) {
-                eh = readlane(sh[0], s);
-                eg_ = readlane(sg[0], s);
-            } else {
-                const int q = s >> 6, l = s & 63;
-                eh = q == 0 ? readlane(sh[0], l) : readlane(sh[NQ - 1], l);
-                eg_ = q == 0 ? readlane(sg[0], l) : readlane(sg[NQ - 1], l);
-            }
-            if (lane == 0) {
-                yh = eh;
-                yg = eg_;
-            }
-        }
-        const int j = s - lane;
-        if (rowok && j >= 0 && j < ncol) {
-            const int c = c0 + j;
-            const size_t i = rowbase + j;
-            const double pu = io.p0[i], pv = io.p1[i];
-            const double ax = cf.alpha * cf.inv_dx[c];
-            const double sl = c == 0 ? cf.src[0] + lb : cf.src[c];
-            const MarchCell::Pre p = MarchCell::pre(cf, ax, ay, sl, pu, pv);
-            double nu, nv;
-            MarchCell::step(p, 0.5 * ax, hy, xf, xh, yh, yg, nu, nv);
-            io.o0[i] = nu;
-            io.o1[i] = nv;
-            yho = yh;
-            ygo = yg;
-            if (lane == nrow - 1) {
-                nout[j] = yh;
-                nout[TW + j] = yg;
-            }
-        }
-    }
-    if (rowok) {
-        double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
-        ec[lane] = xf;
-        ec[kWave + lane] = xh;
-    }
-    if (lane == 0) atomicAdd(&eg.counters[pass], 1);
-}
-
-// ---------------------------------------------------------------------------
-// SOLVE cell: exact J(w) delta = rhs, J from exact_jac2D (C/hypernet2D.py:2627).
-// Linearised outflows: east a = ax*u*du, b = 0.5*ax*(v*du + u*dv);
-// north c = 0.5*ay*(v*du + u*dv), d = ay*v*dv.  Same op order as
-// orc_block_solve.
-template <int TW>
-__global__ __launch_bounds__(64) void solve_pass_kernel(Coeffs cf, Engine eg,
-                                                        const double *w, const double *rhs,
-                                                        double *delta, int pass)
-{
-    const int t = blockIdx.x;
-    if (pass > 1 && eg.counters[pass - 1] == 0) return;
-    const int lane = threadIdx.x;
-    const int I = t / eg.ntj, J = t - I * eg.ntj;
-    const int nx = cf.nx, ny = cf.ny;
-    const size_t n = (size_t)nx * ny;
-    const int r0 = I * kWave, c0 = J * TW;
-    const int nrow = min(kWave, ny - r0), ncol = min(TW, nx - c0);
-    const bool rowok = lane < nrow;
-    const int r = r0 + (rowok ? lane : nrow - 1);
-    const int cur = pass & 1, prv = cur ^ 1;
-    constexpr int NQ = TW / kWave;
-
-    double wa = 0.0, wb = 0.0;  // west inflow (pass 1 guess: 0)
-    double sc[NQ], sd[NQ];
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) sc[q] = sd[q] = 0.0;
-    if (pass > 1) {
-        if (J > 0) {
-            const double *e = eg.eb[prv] + (size_t)(t - 1) * 2 * kWave;
-            wa = e[lane];
-            wb = e[kWave + lane];
-        }
-        if (I > 0) {
-            const double *nn = eg.nb[prv] + (size_t)(t - eg.ntj) * 2 * TW;
-#pragma unroll
-            for (int q = 0; q < NQ; ++q) {
-                const int col = lane + kWave * q;
-                if (col < ncol) {
-                    sc[q] = nn[col];
-                    sd[q] = nn[TW + col];
+            if (col >= ncol) continue;
+            if (I > 0) {
+                if (pass == 1) {
+                    C::guess_n(cf, io, r0 - 1, c0 + col, sn0[q], sn1[q]);
+                } else {
+                    const double *nn = eg.nb[prv] + (size_t)(t - eg.ntj) * 2 * TW;
+                    sn0[q] = nn[col];
+                    sn1[q] = nn[TW + col];
+                }
+            } else if (eg.halo_flux != nullptr) {
+                if (pass == 1) {
+                    C::guess_halo(cf, eg, c0 + col, sn0[q], sn1[q]);
+                } else {
+                    sn0[q] = eg.halo_flux[c0 + col];
+                    sn1[q] = eg.halo_flux[nx + c0 + col];
                 }
             }
         }
-    }
-    double *wu = eg.wused + (size_t)t * 2 * kWave;
-    double *su = eg.sused + (size_t)t * 2 * TW;
-    if (pass > 1) {
-        bool mv = rowok && (moved(wa, wu[lane], eg.tol) || moved(wb, wu[kWave + lane], eg.tol));
+        // skip test: march again only if some inflow moved since last used
+        bool need = true;
+        if (pass > 1) {
+            bool mv = rowok &&
+                      (moved(we0, wu[lane], eg.tol) || moved(we1, wu[kWave + lane], eg.tol));
 #pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-            const int col = lane + kWave * q;
-            if (col < ncol)
-                mv = mv || moved(sc[q], su[col], eg.tol) || moved(sd[q], su[TW + col], eg.tol);
+            for (int q = 0; q < NQ; ++q) {
+                const int col = lane + kWave * q;
+                if (col < ncol)
+                    mv = mv || moved(sn0[q], su[col], eg.tol) ||
+                         moved(sn1[q], su[TW + col], eg.tol);
+            }
+            need = __any(mv);
         }
-        if (!__any(mv)) {
+        if (lane == 0) sm.need = need;
+    }
+    __syncthreads();
+    const bool need = sm.need;
+    if (!need) {
+        if (wave == 0) {  // carry this tile's outflow into the current generation
             const double *ep = eg.eb[prv] + (size_t)t * 2 * kWave;
             double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
             ec[lane] = ep[lane];
@@ -321,141 +287,253 @@ __global__ __launch_bounds__(64) void solve_pass_kernel(Coeffs cf, Engine eg,
             double *nc = eg.nb[cur] + (size_t)t * 2 * TW;
 #pragma unroll
             for (int q = 0; q < 2 * NQ; ++q) nc[lane + kWave * q] = np_[lane + kWave * q];
-            return;
+        }
+        __syncthreads();  // sm reused by the next tile
+        return false;
+    }
+
+    // ---- stage the tile's inputs: coalesced row segments -> LDS [row][col]
+    const size_t tbase = (size_t)r0 * nx + c0;
+    for (int e = tid; e < kWave * TW; e += kThreads) {
+        const int rr = e / TW, cc = e - rr * TW;
+        if (rr < nrow && cc < ncol) {
+            const size_t g = tbase + (size_t)rr * nx + cc;
+#pragma unroll
+            for (int q = 0; q < C::NIN; ++q) sm.x[q][e] = io.in[q][g];
         }
     }
-    if (rowok) {
-        wu[lane] = wa;
-        wu[kWave + lane] = wb;
+    for (int cc = tid; cc < TW; cc += kThreads) {
+        const int c = c0 + min(cc, ncol - 1);
+        sm.dx[cc] = cf.inv_dx[c];
+        sm.src[cc] = cf.src[c];
     }
+    if (wave == 0) {
+        if (rowok) {
+            wu[lane] = we0;
+            wu[kWave + lane] = we1;
+        }
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-        const int col = lane + kWave * q;
-        if (col < ncol) {
-            su[col] = sc[q];
-            su[TW + col] = sd[q];
+        for (int q = 0; q < NQ; ++q) {
+            const int col = lane + kWave * q;
+            if (col < ncol) {
+                su[col] = sn0[q];
+                su[TW + col] = sn1[q];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- wave 0: skewed sweep, lane l marches row r0+l, column j = s - l.
+    // Only LDS and registers inside the loop; the next step's operands are
+    // read one step ahead so the LDS latency hides under the cell's math.
+    if (wave == 0) {
+        const typename C::Row rw = C::row(cf, r);
+        double e0 = we0, e1 = we1;    // running west inflow of my row
+        double no0 = 0.0, no1 = 0.0;  // my last north outflow (for lane + 1)
+        const int nsteps = ncol + nrow - 1;
+        double *lrow[C::NIN];
+#pragma unroll
+        for (int q = 0; q < C::NIN; ++q) lrow[q] = sm.x[q] + lane * TW;
+        double xn[C::NIN], dxn, scn;
+        {
+            const int jn = min(max(-lane, 0), ncol - 1);
+#pragma unroll
+            for (int q = 0; q < C::NIN; ++q) xn[q] = lrow[q][jn];
+            dxn = sm.dx[jn];
+            scn = sm.src[jn];
+        }
+        for (int s = 0; s < nsteps; ++s) {
+            double xc[C::NIN];
+#pragma unroll
+            for (int q = 0; q < C::NIN; ++q) xc[q] = xn[q];
+            const double dxc = dxn, scc = scn;
+            {
+                const int jn = min(max(s + 1 - lane, 0), ncol - 1);
+#pragma unroll
+                for (int q = 0; q < C::NIN; ++q) xn[q] = lrow[q][jn];
+                dxn = sm.dx[jn];
+                scn = sm.src[jn];
+            }
+            double n0 = shr1(no0), n1 = shr1(no1);
+            if (s < ncol) {  // lane 0 takes the tile's south edge for column s
+                double a, b;
+                if constexpr (NQ == 1) {
+                    a = readlane(sn0[0], s);
+                    b = readlane(sn1[0], s);
+                } else {
+                    const int l = s & 63;
+                    a = (s >> 6) == 0 ? readlane(sn0[0], l) : readlane(sn0[NQ - 1], l);
+                    b = (s >> 6) == 0 ? readlane(sn1[0], l) : readlane(sn1[NQ - 1], l);
+                }
+                if (lane == 0) {
+                    n0 = a;
+                    n1 = b;
+                }
+            }
+            const int j = s - lane;
+            if (rowok && j >= 0 && j < ncol) {
+                double o0, o1;
+                C::cell(cf, rw, xc, dxc, scc, c0 + j, e0, e1, n0, n1, o0, o1);
+                lrow[0][j] = o0;
+                lrow[1][j] = o1;
+                no0 = n0;
+                no1 = n1;
+                if (lane == nrow - 1) {
+                    sm.nout[0][j] = n0;
+                    sm.nout[1][j] = n1;
+                }
+            }
+        }
+        if (rowok) {
+            double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
+            ec[lane] = e0;
+            ec[kWave + lane] = e1;
+        }
+    }
+    __syncthreads();
+    {
+        double *nout = eg.nb[cur] + (size_t)t * 2 * TW;
+        for (int cc = tid; cc < ncol; cc += kThreads) {
+            nout[cc] = sm.nout[0][cc];
+            nout[TW + cc] = sm.nout[1][cc];
         }
     }
 
-    const double ay = cf.alpha * cf.inv_dy[r];
-    double ea = wa, eb = wb;
-    double nco = 0.0, ndo = 0.0;
-    double *nout = eg.nb[cur] + (size_t)t * 2 * TW;
-    const int nsteps = ncol + nrow - 1;
-    const size_t rowbase = (size_t)r * nx + c0;
-    for (int s = 0; s < nsteps; ++s) {
-        double ic = shr1(nco), id = shr1(ndo);
-        if (s < ncol) {
-            double e0, e1;
-            if constexpr (NQ == 1) {
-                e0 = readlane(sc[0], s);
-                e1 = readlane(sd[0], s);
-            } else {
-                const int q = s >> 6, l = s & 63;
-                e0 = q == 0 ? readlane(sc[0], l) : readlane(sc[NQ - 1], l);
-                e1 = q == 0 ? readlane(sd[0], l) : readlane(sd[NQ - 1], l);
-            }
-            if (lane == 0) {
-                ic = e0;
-                id = e1;
-            }
-        }
-        const int j = s - lane;
-        if (rowok && j >= 0 && j < ncol) {
-            const int c = c0 + j;
-            const size_t i = rowbase + j;
-            const double u = w[i], v = w[n + i];
-            const double ax = cf.alpha * cf.inv_dx[c];
-            const double eu = (rhs[i] + ea) + ic;
-            const double ev = (rhs[n + i] + eb) + id;
-            const double a00 = (1.0 + ax * u) + (0.5 * ay) * v;
-            const double a01 = (0.5 * ay) * u;
-            const double a10 = (0.5 * ax) * v;
-            const double a11 = (1.0 + ay * v) + (0.5 * ax) * u;
-            const double det = a00 * a11 - a01 * a10;
-            const double du = (a11 * eu - a01 * ev) / det;
-            const double dv = (a00 * ev - a10 * eu) / det;
-            delta[i] = du;
-            delta[n + i] = dv;
-            const double m = v * du + u * dv;
-            ea = (ax * u) * du;
-            eb = (0.5 * ax) * m;
-            nco = (0.5 * ay) * m;
-            ndo = (ay * v) * dv;
-            if (lane == nrow - 1) {
-                nout[j] = nco;
-                nout[TW + j] = ndo;
-            }
+    // ---- write the outputs back, coalesced
+    for (int e = tid; e < kWave * TW; e += kThreads) {
+        const int rr = e / TW, cc = e - rr * TW;
+        if (rr < nrow && cc < ncol) {
+            const size_t g = tbase + (size_t)rr * nx + cc;
+            io.out[0][g] = sm.x[0][e];
+            io.out[1][g] = sm.x[1][e];
         }
     }
-    if (rowok) {
-        double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
-        ec[lane] = ea;
-        ec[kWave + lane] = eb;
-    }
-    if (lane == 0) atomicAdd(&eg.counters[pass], 1);
+    __syncthreads();  // sm reused by the next tile
+    return true;
 }
 
-// One thread: fold the pass counters of the step into the run statistics and
-// reset them for the next step.  Pass k "confirms" the step when it marched
-// no tile; a step whose every allowed pass still marched tiles is counted as
-// unconverged (only possible when max_passes is set below the guaranteed
-// bound of #tile-anti-diagonals + 1).
-__global__ void pass_epilogue_kernel(int *counters, int kmax, DevStats *stats)
+template <class C, int TW>
+__global__ __launch_bounds__(kThreads) void pass_kernel(Coeffs cf, Engine eg, typename C::Io io,
+                                                        int pass)
 {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    long long tiles = 0;
-    int used = 0;
-    for (int k = 1; k <= kmax; ++k) {
-        const int ck = counters[k];
-        tiles += ck;
-        if (used == 0 && ck == 0) used = k;
-        counters[k] = 0;
+    __shared__ TileLds<C, TW> sm;
+    if (pass > 1 && eg.counters[pass - 1] == 0) return;  // converged already
+    if (tile_pass<C, TW>(cf, eg, io, blockIdx.x, pass, sm) && threadIdx.x == 0)
+        atomicAdd(&eg.counters[pass], 1);
+}
+
+// FINAL pass (pass = P+1): all tiles check/march once; the last workgroup to
+// arrive continues alone with passes P+2, P+3, ... until a pass marches
+// nothing (the bound #tile anti-diagonals + 1 guarantees termination), then
+// folds the step's counters into the run statistics and resets them.
+template <class C, int TW>
+__global__ __launch_bounds__(kThreads) void final_kernel(Coeffs cf, Engine eg, typename C::Io io,
+                                                         int pass, DevStats *stats)
+{
+    __shared__ TileLds<C, TW> sm;
+    const bool live = !(pass > 1 && eg.counters[pass - 1] == 0);
+    if (live && tile_pass<C, TW>(cf, eg, io, blockIdx.x, pass, sm) && threadIdx.x == 0)
+        atomicAdd(&eg.counters[pass], 1);
+    // arrival: every storing wave drains, then one release and the ticket
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int tk = atomicAdd(eg.ticket, 1);
+        last = (tk == (int)gridDim.x - 1);
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
     }
-    if (used == 0) {
-        stats->unconverged_steps += 1;
-        used = kmax;
+    __syncthreads();
+    if (!last) return;
+
+    const int ntiles = eg.nti * eg.ntj;
+    int k = pass;
+    int moved_last = live ? __hip_atomic_load(&eg.counters[k], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : 0;
+    int tail = 0;
+    __shared__ int cnt;
+    while (moved_last != 0 && k < eg.kbound) {
+        ++k;
+        ++tail;
+        if (threadIdx.x == 0) cnt = 0;
+        __syncthreads();
+        for (int t = 0; t < ntiles; ++t)
+            if (tile_pass<C, TW>(cf, eg, io, t, k, sm) && threadIdx.x == 0) ++cnt;
+        // pass k's edges (stored by one lane, read by others next pass)
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __syncthreads();
+        moved_last = cnt;
+        if (threadIdx.x == 0) eg.counters[k] = cnt;
     }
-    stats->tile_marches += tiles;
-    stats->steps += 1;
-    stats->passes += used;
-    if (used > stats->max_passes) stats->max_passes = used;
+    if (threadIdx.x == 0) {
+        long long tiles = 0;
+        int used = 0;
+        for (int q = 1; q <= k; ++q) {
+            const int cq = __hip_atomic_load(&eg.counters[q], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+            tiles += cq;
+            if (used == 0 && cq == 0) used = q;
+            eg.counters[q] = 0;
+        }
+        if (used == 0) {  // hit the bound (cannot happen: see DESIGN.md section 4)
+            stats->unconverged_steps += 1;
+            used = k;
+        }
+        stats->tile_marches += tiles;
+        stats->steps += 1;
+        stats->passes += used;
+        stats->tail_passes += tail;
+        if (used > stats->max_passes) stats->max_passes = used;
+        // the engine keeps the generation parity of the final outflow
+        *eg.ticket = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    }
+}
+
+template <class C>
+int launch_pass(const Coeffs &cf, const Engine &eg, const typename C::Io &io, int pass,
+                bool final, DevStats *stats, hipStream_t st)
+{
+    const dim3 grid(eg.nti * eg.ntj), block(kThreads);
+    if (eg.tw == 64) {
+        if (final)
+            final_kernel<C, 64><<<grid, block, 0, st>>>(cf, eg, io, pass, stats);
+        else
+            pass_kernel<C, 64><<<grid, block, 0, st>>>(cf, eg, io, pass);
+    } else if constexpr (C::NIN * 128 * kWave * 8 <= 160 * 1024) {
+        if (eg.tw != 128) return -1;
+        if (final)
+            final_kernel<C, 128><<<grid, block, 0, st>>>(cf, eg, io, pass, stats);
+        else
+            pass_kernel<C, 128><<<grid, block, 0, st>>>(cf, eg, io, pass);
+    } else {
+        return -1;  // LDS budget: the 4-plane SOLVE cell needs tile_w = 64
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 }  // namespace
 
 int launch_march_pass(const Coeffs &cf, const Engine &eg, const double *wp, double *w,
-                      int pass, hipStream_t st)
+                      int pass, bool final, DevStats *stats, hipStream_t st)
 {
     const size_t n = (size_t)cf.nx * cf.ny;
-    MarchCell::In io{wp, wp + n, w, w + n};
-    const dim3 grid(eg.nti * eg.ntj), block(kWave);
-    if (eg.tw == 64)
-        march_pass_kernel<64><<<grid, block, 0, st>>>(cf, eg, io, pass);
-    else if (eg.tw == 128)
-        march_pass_kernel<128><<<grid, block, 0, st>>>(cf, eg, io, pass);
-    else
-        return -1;
-    return hipGetLastError() == hipSuccess ? 0 : -3;
+    MarchCell::Io io{{wp, wp + n}, {w, w + n}};
+    return launch_pass<MarchCell>(cf, eg, io, pass, final, stats, st);
 }
 
-int launch_solve_pass(const Coeffs &cf, const Engine &eg, const double *w,
-                      const double *rhs, double *delta, int pass, hipStream_t st)
+int launch_solve_pass(const Coeffs &cf, const Engine &eg, const double *w, const double *rhs,
+                      double *delta, int pass, bool final, DevStats *stats, hipStream_t st)
 {
-    const dim3 grid(eg.nti * eg.ntj), block(kWave);
-    if (eg.tw == 64)
-        solve_pass_kernel<64><<<grid, block, 0, st>>>(cf, eg, w, rhs, delta, pass);
-    else if (eg.tw == 128)
-        solve_pass_kernel<128><<<grid, block, 0, st>>>(cf, eg, w, rhs, delta, pass);
-    else
-        return -1;
-    return hipGetLastError() == hipSuccess ? 0 : -3;
-}
-
-int launch_pass_epilogue(const Engine &eg, int kmax, DevStats *stats, hipStream_t st)
-{
-    pass_epilogue_kernel<<<1, 64, 0, st>>>(eg.counters, kmax, stats);
-    return hipGetLastError() == hipSuccess ? 0 : -3;
+    const size_t n = (size_t)cf.nx * cf.ny;
+    SolveCell::Io io{{w, w + n, rhs, rhs + n}, {delta, delta + n}};
+    return launch_pass<SolveCell>(cf, eg, io, pass, final, stats, st);
 }
 
 }  // namespace burg

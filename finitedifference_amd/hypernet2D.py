@@ -19,7 +19,7 @@ reference module ``hypernet2D`` for the FOM path (paths relative to
 The snapshot matrix is the reference's: float64, shape (2*nx*ny,
 num_steps + 1), C-contiguous, column j = state after j steps, u rows then v
 rows.  Extensions are keyword-only (solver, snap_every, device, tile_w, tol,
-max_passes, verbose, allow_nonsquare) and default to reference behaviour.
+par_passes, verbose, allow_nonsquare) and default to reference behaviour.
 """
 import glob
 import os
@@ -66,7 +66,7 @@ def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
 
 def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
                                 snap_every=1, device=0, tile_w=64, tol=DEFAULT_TOL,
-                                max_passes=0, verbose=1, allow_nonsquare=False,
+                                par_passes=0, verbose=1, allow_nonsquare=False,
                                 newton_max_its=100, newton_rtol=1e-12, return_stats=False):
     """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM
     (C/hypernet2D.py:72-131) on an MI355X.
@@ -81,7 +81,7 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     if verbose:
         print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mu, device, allow_nonsquare, tile_w=tile_w,
-                   max_passes=max_passes, tol=tol)
+                   par_passes=par_passes, tol=tol)
     snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
                                      solver, newton_max_its, newton_rtol, int(snap_every))
     if verbose >= 2:

@@ -19,7 +19,7 @@ DEFAULT_TOL = 2.0 ** -50  # 4 ulp relative inflow motion
 class FOMContext:
     """A grid (nx x ny) resident on one GPU."""
 
-    def __init__(self, nx, ny, device=0, tile_w=64, max_passes=0, tol=DEFAULT_TOL,
+    def __init__(self, nx, ny, device=0, tile_w=64, par_passes=0, tol=DEFAULT_TOL,
                  profile=False):
         self._L = _lib.load()
         self.nx, self.ny, self.device = int(nx), int(ny), int(device)
@@ -27,7 +27,7 @@ class FOMContext:
         _lib.check(self._L.burg_ctx_create(self.device, self.nx, self.ny, ctypes.byref(h)))
         self._h = h
         self._problem = None
-        self.set_options(tile_w, max_passes, tol, profile)
+        self.set_options(tile_w, par_passes, tol, profile)
 
     @property
     def m(self):
@@ -44,10 +44,10 @@ class FOMContext:
         except Exception:
             pass
 
-    def set_options(self, tile_w=64, max_passes=0, tol=DEFAULT_TOL, profile=False):
-        _lib.check(self._L.burg_set_options(self._h, int(tile_w), int(max_passes), float(tol),
+    def set_options(self, tile_w=64, par_passes=0, tol=DEFAULT_TOL, profile=False):
+        _lib.check(self._L.burg_set_options(self._h, int(tile_w), int(par_passes), float(tol),
                                             1 if profile else 0))
-        self.options = dict(tile_w=tile_w, max_passes=max_passes, tol=tol, profile=profile)
+        self.options = dict(tile_w=tile_w, par_passes=par_passes, tol=tol, profile=profile)
 
     def set_problem(self, grid_x, grid_y, dt, mu, allow_nonsquare=False):
         key = (np.asarray(grid_x).tobytes(), np.asarray(grid_y).tobytes(), float(dt),

@@ -66,12 +66,13 @@ typedef struct burg_stats {
     int32_t unconverged_steps;  /* steps that hit the pass cap; 0 on success */
     int64_t newton_updates;     /* newton solver: total Newton updates */
     int32_t newton_max_updates; /* newton solver: most updates in one step */
-    int32_t reserved;
+    int32_t par_passes;         /* parallel passes launched per step (engine option) */
     double loop_ms;             /* device time of the time loop (HIP events) */
     double flush_ms;            /* device time of snapshot transpose + D2H */
     double march_kernel_ms;     /* profiling mode: summed march kernel time */
     int64_t march_launches;     /* profiling mode: march kernel launches timed */
     double last_rel;            /* newton solver: last step's final ||R||/||R0|| */
+    int64_t tail_passes;        /* passes finished by the final kernel's last workgroup */
 } burg_stats;
 
 int burg_abi_version(void);
@@ -100,11 +101,13 @@ int burg_set_problem(burg_ctx *ctx, const double *inv_dx, const double *inv_dy,
                      const double *src, const double *lbc, double dt);
 
 /* Engine options.  tile_w: tile width in cells (64 or 128; tile height is the
- * 64-lane wavefront).  max_passes: Jacobi pass cap per step (<= 0: the
- * guaranteed bound, #tile anti-diagonals + 1).  tol: relative inflow change
- * below which a tile is not re-marched (0 = bitwise fixed point).
+ * 64-lane wavefront).  par_passes: block-Jacobi passes launched over all
+ * tiles per step before the final pass (<= 0: default 3); the final pass
+ * always finishes the step at the fixed point, so this only trades launches
+ * against tail work.  tol: relative inflow change below which a tile is not
+ * re-marched (0 = bitwise fixed point = the sequential march).
  * profile: 1 = time every march launch with HIP events (burg_stats). */
-int burg_set_options(burg_ctx *ctx, int tile_w, int max_passes, double tol, int profile);
+int burg_set_options(burg_ctx *ctx, int tile_w, int par_passes, double tol, int profile);
 
 /* Parity hooks (whole-grid host arrays; single-GPU contexts only). */
 int burg_residual(burg_ctx *ctx, const double *w, const double *wp, double *r,

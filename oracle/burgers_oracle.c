@@ -467,3 +467,148 @@ int orc_march_tiled_sim(int nx, int ny, const double *inv_dx, const double *inv_
     if (tiles_done) *tiles_done = done;
     return k;
 }
+
+/* Variant with a time-extrapolated pass-1 guess: g = 2*g_wp - e_prev, where
+ * g_wp is the "neighbour did not move" outflow and e_prev the neighbour's
+ * final outflow of the previous step (second-order in dt).  e_prev buffers
+ * (E: nt*2*th, N: nt*2*tw) are read and then overwritten with this step's
+ * final outflows; pass have_prev = 0 on the first step.                     */
+int orc_march_tiled_sim2(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                         const double *src, const double *lbc, double dt,
+                         const double *wp, double *w, int th, int tw, int kmax,
+                         double tol, long long *tiles_done, double *eprev, double *nprev,
+                         int have_prev, long long *pass_tiles)
+{
+    const size_t n = (size_t)nx * ny;
+    const int nti = (ny + th - 1) / th, ntj = (nx + tw - 1) / tw;
+    const size_t nt = (size_t)nti * ntj;
+    orc_grid g = {inv_dx, inv_dy, src, lbc, 0.5 * dt, nx, ny};
+    double *E = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *Nn = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *E2 = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *N2 = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *Wu = (double *)calloc(nt * 2 * th, sizeof(double));
+    double *Su = (double *)calloc(nt * 2 * tw, sizeof(double));
+    double *yh = (double *)malloc(tw * sizeof(double)), *yg = (double *)malloc(tw * sizeof(double));
+    double *win = (double *)malloc(2 * th * sizeof(double)), *sin_ = (double *)malloc(2 * tw * sizeof(double));
+    long long done = 0;
+    int k;
+    for (k = 1; k <= kmax; ++k) {
+        int any = 0;
+        long long pt = 0;
+        memcpy(E2, E, nt * 2 * th * sizeof(double));
+        memcpy(N2, Nn, nt * 2 * tw * sizeof(double));
+        for (int I = 0; I < nti; ++I)
+            for (int J = 0; J < ntj; ++J) {
+                const size_t t = (size_t)I * ntj + J;
+                const int r0 = I * th, c0 = J * tw;
+                const int r1 = r0 + th < ny ? r0 + th : ny, c1 = c0 + tw < nx ? c0 + tw : nx;
+                for (int c = c0; c < c1; ++c) {
+                    double sh = 0.0, sg = 0.0;
+                    if (I > 0) {
+                        if (k == 1) {
+                            double bu, bv, xfp, xhp, yhp, ygp;
+                            const size_t i = IDX(r0 - 1, c, nx);
+                            const double pu = wp[i], pv = wp[n + i];
+                            cell_pre(&g, r0 - 1, c, pu, pv, &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                            const double hy = 0.5 * (g.a * inv_dy[r0 - 1]);
+                            sh = fma(hy * pu, pv, yhp);
+                            sg = fma(hy * pv, pv, ygp);
+                            if (have_prev) {
+                                const double *pn = nprev + (t - ntj) * 2 * tw;
+                                sh = 2.0 * sh - pn[c - c0];
+                                sg = 2.0 * sg - pn[tw + c - c0];
+                            }
+                        } else {
+                            const double *sn = N2 + (t - ntj) * 2 * tw;
+                            sh = sn[c - c0];
+                            sg = sn[tw + c - c0];
+                        }
+                    }
+                    sin_[c - c0] = sh;
+                    sin_[tw + c - c0] = sg;
+                }
+                for (int r = r0; r < r1; ++r) {
+                    double xf = 0.0, xh = 0.0;
+                    if (J > 0) {
+                        if (k == 1) {
+                            double bu, bv, xfp, xhp, yhp, ygp;
+                            const size_t i = IDX(r, c0 - 1, nx);
+                            const double pu = wp[i], pv = wp[n + i];
+                            cell_pre(&g, r, c0 - 1, pu, pv, &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                            const double hx = 0.5 * (g.a * inv_dx[c0 - 1]);
+                            xf = fma(hx * pu, pu, xfp);
+                            xh = fma(hx * pu, pv, xhp);
+                            if (have_prev) {
+                                const double *pe = eprev + (t - 1) * 2 * th;
+                                xf = 2.0 * xf - pe[r - r0];
+                                xh = 2.0 * xh - pe[th + r - r0];
+                            }
+                        } else {
+                            const double *se = E2 + (t - 1) * 2 * th;
+                            xf = se[r - r0];
+                            xh = se[th + r - r0];
+                        }
+                    }
+                    win[r - r0] = xf;
+                    win[th + r - r0] = xh;
+                }
+                int need = (k == 1);
+                if (!need) {
+                    double *wu = Wu + t * 2 * th, *su = Su + t * 2 * tw;
+                    for (int r = 0; r < r1 - r0 && !need; ++r)
+                        need = moved(win[r], wu[r], tol) || moved(win[th + r], wu[th + r], tol);
+                    for (int c = 0; c < c1 - c0 && !need; ++c)
+                        need = moved(sin_[c], su[c], tol) || moved(sin_[tw + c], su[tw + c], tol);
+                }
+                if (!need) continue;
+                any = 1;
+                ++done;
+                ++pt;
+                memcpy(Wu + t * 2 * th, win, 2 * th * sizeof(double));
+                memcpy(Su + t * 2 * tw, sin_, 2 * tw * sizeof(double));
+                for (int c = c0; c < c1; ++c) {
+                    yh[c - c0] = sin_[c - c0];
+                    yg[c - c0] = sin_[tw + c - c0];
+                }
+                double *eo = E + t * 2 * th, *no = Nn + t * 2 * tw;
+                for (int r = r0; r < r1; ++r) {
+                    double xfw = win[r - r0], xhw = win[th + r - r0];
+                    const double ay = g.a * inv_dy[r], hy = 0.5 * ay;
+                    for (int c = c0; c < c1; ++c) {
+                        const size_t i = IDX(r, c, nx);
+                        const double hx = 0.5 * (g.a * inv_dx[c]);
+                        double bu, bv, xfp, xhp, yhp, ygp;
+                        cell_pre(&g, r, c, wp[i], wp[n + i], &bu, &bv, &xfp, &xhp, &yhp, &ygp);
+                        const double cu = (bu + xfw) + yh[c - c0];
+                        const double cv = (bv + yg[c - c0]) + xhw;
+                        const double mm = fma(hx, cu, hy * cv);
+                        const double s = 0.5 + sqrt(0.25 + mm);
+                        const double rs = 1.0 / s;
+                        const double nu = cu * rs, nv = cv * rs;
+                        const double hxu = hx * nu;
+                        xfw = fma(hxu, nu, xfp);
+                        xhw = fma(hxu, nv, xhp);
+                        yh[c - c0] = fma(hy * nu, nv, yhp);
+                        yg[c - c0] = fma(hy * nv, nv, ygp);
+                        w[i] = nu;
+                        w[n + i] = nv;
+                    }
+                    eo[r - r0] = xfw;
+                    eo[th + r - r0] = xhw;
+                }
+                for (int c = c0; c < c1; ++c) {
+                    no[c - c0] = yh[c - c0];
+                    no[tw + c - c0] = yg[c - c0];
+                }
+            }
+        if (pass_tiles && k <= 16) pass_tiles[k - 1] = pt;
+        if (!any) break;
+    }
+    memcpy(eprev, E, nt * 2 * th * sizeof(double));
+    memcpy(nprev, Nn, nt * 2 * tw * sizeof(double));
+    free(E); free(Nn); free(E2); free(N2); free(Wu); free(Su);
+    free(yh); free(yg); free(win); free(sin_);
+    if (tiles_done) *tiles_done = done;
+    return k;
+}

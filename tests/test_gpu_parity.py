@@ -78,25 +78,28 @@ def test_block_solve_matches_spsolve(gpu, orc, N):
 
 
 # ------------------------------------------------------------------ march --
-@pytest.mark.parametrize("N,tw", [(13, 64), (64, 64), (100, 64), (250, 64), (250, 128),
-                                  (300, 128)])
-def test_march_step_bitwise_sequential(gpu, orc, N, tw):
-    """tol = 0: the tile engine's fixed point is the sequential march."""
+@pytest.mark.parametrize("N,tw,par", [(13, 64, 3), (64, 64, 3), (100, 64, 3), (250, 64, 3),
+                                      (250, 128, 3), (300, 128, 3), (300, 64, 1)])
+def test_march_step_bitwise_sequential(gpu, orc, N, tw, par):
+    """tol = 0: the tile engine's fixed point is the sequential march (needs
+    ~#tile rows passes in y-uniform regions: exercises the tail path)."""
     P = orc.Problem(N)
     wp = state_after(orc, P, 7)
-    ctx = make_ctx(N, tile_w=tw, tol=0.0)
+    ctx = make_ctx(N, tile_w=tw, tol=0.0, par_passes=par)
     snaps, st, its, _ = ctx.run(wp, 1)
     assert st["unconverged_steps"] == 0
     assert np.array_equal(snaps[:, 1], P.march_step(wp))
 
 
-@pytest.mark.parametrize("N,tw", [(250, 64), (333, 64), (512, 128)])
-def test_march_step_bitwise_tiled_schedule(gpu, orc, N, tw):
+@pytest.mark.parametrize("N,tw,par", [(250, 64, 3), (333, 64, 3), (512, 128, 3), (333, 64, 1),
+                                      (512, 64, 2)])
+def test_march_step_bitwise_tiled_schedule(gpu, orc, N, tw, par):
     """tol = 4 ulp: the GPU reproduces the CPU schedule simulator bit for bit,
-    and both sit within ~1e-16 of the sequential march."""
+    and both sit within ~1e-16 of the sequential march.  par < 3 leaves passes
+    to the final kernel's last workgroup (the tail path)."""
     P = orc.Problem(N)
     wp = state_after(orc, P, 20)
-    ctx = make_ctx(N, tile_w=tw, tol=TOL4ULP)
+    ctx = make_ctx(N, tile_w=tw, tol=TOL4ULP, par_passes=par)
     snaps, st, its, _ = ctx.run(wp, 1)
     ws, k, _ = P.march_tiled(wp, tw=tw, tol=TOL4ULP)
     assert np.array_equal(snaps[:, 1], ws)
