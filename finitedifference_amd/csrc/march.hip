@@ -1,7 +1,7 @@
 // march.hip -- the upwind tile engine: one implicit time step of the 2D
 // inviscid Burgers FOM (MARCH cell) and the exact Newton linear solve
 // J(w) delta = rhs (SOLVE cell), both as a skewed-wavefront sweep over
-// 64-row tiles with block-Jacobi passes between tiles (DESIGN.md sections 3-4).
+// 64-row tiles with block-Jacobi passes between tiles (DESIGN.md sections 3-5).
 //
 // Why a march: the reference residual (C/hypernet2D.py:2512-2570) couples a
 // cell only to itself, its west (r, c-1) and south (r-1, c) neighbours, so
@@ -16,31 +16,73 @@
 // (orc_march_step / orc_block_solve / orc_march_tiled_sim) and the GPU result
 // is compared against it (bitwise for equal tiling and tolerance).
 //
-// Schedule per step: passes 1..P are launched over all tiles (one wavefront
+// Schedule per step: passes 1..P are launched over all tiles (one workgroup
 // per tile, block Jacobi between tiles); pass P+1 is the FINAL kernel: every
 // tile checks its inflow, and the last workgroup to finish (arrival ticket,
 // agent-scope release/acquire) runs any further passes itself until no tile
 // moves -- so a step always ends at the fixed point, with no host round trip
 // and no idle launches.  It also folds the step's statistics.
+//
+// Inside a tile the critical path is the skewed sweep: 64 + 64 - 1 dependent
+// steps of one wavefront.  A lone wave issues about one VALU instruction per
+// 4-5 cycles whatever the instruction (measured), so the
+// sweeping wave executes only the cell chain, the DPP hand-over and its
+// commits; a helper wave on another SIMD precomputes the inflow-independent
+// part of each cell into an LDS ring a few diagonals ahead.
 #include "burg_internal.h"
+
+#ifdef BURG_STAMPS
+__device__ long long burg_stamp[4];
+#endif
 
 namespace burg {
 namespace {
 
-
+// lane i <- lane i-1 over the whole wave (DPP wave_shr:1); lane 0 gets +0.0
+// (bound_ctrl).  Must run with every lane enabled: a DPP read from a
+// disabled lane does not return that lane's register.
 __device__ __forceinline__ double shr1(double x)
 {
-    // lane i <- lane i-1 (wave-wide DPP shift; lane 0 keeps 0)
-    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), 0x138, 0xf, 0xf, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), 0x138, 0xf, 0xf, false);
+    const int lo = __builtin_amdgcn_mov_dpp(__double2loint(x), 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(x), 0x138, 0xf, 0xf, true);
     return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double readlane(double x, int l)
+// Correctly rounded sqrt(q) for normal q, without the denormal/special-case
+// range scaling of the compiler's expansion: the same v_rsq_f64 seed,
+// Goldschmidt step and two Newton corrections (gfx950 ISA as emitted for
+// sqrt()), hence bit-identical to IEEE sqrt on [2^-900, 2^900) (a negative
+// q gives NaN, as sqrt does).
+__device__ __forceinline__ double sqrt_normal(double q)
 {
-    const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
-    const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
-    return __hiloint2double(hi, lo);
+    const double y = __builtin_amdgcn_rsq(q);
+    double g = q * y;
+    double h = y * 0.5;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, q);
+    g = fma(d, h, g);
+    d = fma(-g, g, q);
+    return fma(d, h, g);
+}
+
+// a0/b and a1/b correctly rounded, sharing the reciprocal refinement: the
+// compiler's division expansion (v_rcp_f64 seed, two Newton steps, one
+// Markstein correction) without v_div_scale/fmas/fixup, which are identities
+// for normal operands (b in [1, 2^900], a = 0 or |a| >= 2^-900).
+__device__ __forceinline__ void div2_normal(double a0, double a1, double b, double &q0,
+                                            double &q1)
+{
+    double r = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-b, r, 1.0);
+    r = fma(r, e, r);
+    const double t0 = a0 * r, t1 = a1 * r;
+    const double m0 = fma(-b, t0, a0), m1 = fma(-b, t1, a1);
+    q0 = fma(m0, r, t0);
+    q1 = fma(m1, r, t1);
 }
 
 __device__ __forceinline__ bool moved(double a, double b, double tol)
@@ -70,34 +112,66 @@ struct MarchCell {
         w.lb = cf.lbc[r];
         return w;
     }
-    // solve cell (r, c) given west (e0=XF, e1=XH) and south (n0=YH, n1=YG)
-    // inflow; the inflow registers are overwritten with this cell's outflow.
-    __device__ static void cell(const Coeffs &cf, const Row &rw, const double (&x)[NIN],
-                                double invdx, double srcc, int c, double &e0, double &e1,
-                                double &n0, double &n1, double &o0, double &o1)
+    // Inflow-independent part of a cell.
+    struct Pre {
+        double hx, xfp, xhp, yhp, ygp, bu, bv;
+    };
+    static constexpr int NPRE = 7;  // Pre fields as staged in the helper ring
+    __device__ static void pack(const Pre &p, double (&f)[NPRE])
     {
+        f[0] = p.hx, f[1] = p.xfp, f[2] = p.xhp, f[3] = p.yhp;
+        f[4] = p.ygp, f[5] = p.bu, f[6] = p.bv;
+    }
+    __device__ static Pre unpack(const double *f)
+    {
+        return Pre{f[0], f[1], f[2], f[3], f[4], f[5], f[6]};
+    }
+    __device__ static Pre pre(const Coeffs &cf, const Row &rw, const double *x, double invdx,
+                              double srcc, bool col0)
+    {
+        Pre p;
         const double pu = x[0], pv = x[1];
         const double ax = cf.alpha * invdx;
-        const double hx = 0.5 * ax;
-        const double sl = c == 0 ? srcc + rw.lb : srcc;
+        p.hx = 0.5 * ax;
+        const double sl = col0 ? srcc + rw.lb : srcc;
         const double hu = 0.5 * pu;
-        const double xfp = ax * (hu * pu);
-        const double xhp = ax * (hu * pv);
-        const double yhp = rw.ay * (hu * pv);
-        const double ygp = rw.ay * ((0.5 * pv) * pv);
-        const double bu = ((pu - xfp) - yhp) + sl;
-        const double bv = (pv - ygp) - xhp;
-        const double cu = (bu + e0) + n0;
-        const double cv = (bv + n1) + e1;
-        const double mm = fma(hx, cu, rw.hy * cv);
-        const double s = 0.5 + sqrt(0.25 + mm);
-        const double rs = 1.0 / s;
-        const double nu = cu * rs, nv = cv * rs;
-        const double hxu = hx * nu;
-        e0 = fma(hxu, nu, xfp);
-        e1 = fma(hxu, nv, xhp);
-        n0 = fma(rw.hy * nu, nv, yhp);
-        n1 = fma(rw.hy * nv, nv, ygp);
+        p.xfp = ax * (hu * pu);
+        p.xhp = ax * (hu * pv);
+        p.yhp = rw.ay * (hu * pv);
+        p.ygp = rw.ay * ((0.5 * pv) * pv);
+        p.bu = ((pu - p.xfp) - p.yhp) + sl;
+        p.bv = (pv - p.ygp) - p.xhp;
+        return p;
+    }
+    // The cell's critical path: west (e0=XF, e1=XH) and south (n0=YH, n1=YG)
+    // inflow -> state (o0, o1) and this cell's outflow.  FAST: the short exact
+    // sequences (range_ok false if an operand is outside their range);
+    // !FAST: the compiler's IEEE sqrt and division.
+    template <bool FAST>
+    __device__ static void chain(const Pre &p, const Row &rw, double e0, double e1, double n0,
+                                 double n1, double &oe0, double &oe1, double &on0, double &on1,
+                                 double &o0, double &o1, bool &range_ok)
+    {
+        const double cu = (p.bu + e0) + n0;
+        const double cv = (p.bv + n1) + e1;
+        const double mm = fma(p.hx, cu, rw.hy * cv);
+        const double q = 0.25 + mm;
+        double s, nu, nv;
+        if constexpr (FAST) {
+            range_ok = fmin(fabs(cu), fabs(cv)) >= 0x1p-900 && fabs(cu) <= 0x1p+900;
+            s = 0.5 + sqrt_normal(q);
+            div2_normal(cu, cv, s, nu, nv);
+        } else {
+            range_ok = true;
+            s = 0.5 + sqrt(q);
+            nu = cu / s;
+            nv = cv / s;
+        }
+        const double hxu = p.hx * nu;
+        oe0 = fma(hxu, nu, p.xfp);
+        oe1 = fma(hxu, nv, p.xhp);
+        on0 = fma(rw.hy * nu, nv, p.yhp);
+        on1 = fma(rw.hy * nv, nv, p.ygp);
         o0 = nu;
         o1 = nv;
     }
@@ -146,28 +220,58 @@ struct SolveCell {
         double ay;
     };
     __device__ static Row row(const Coeffs &cf, int r) { return Row{cf.alpha * cf.inv_dy[r]}; }
-    __device__ static void cell(const Coeffs &cf, const Row &rw, const double (&x)[NIN],
-                                double invdx, double, int, double &e0, double &e1, double &n0,
-                                double &n1, double &o0, double &o1)
+    struct Pre {
+        double ru, rv, a00, a01, a10, a11, det, axu, hax, hay, ayv, u, v;
+    };
+    static constexpr int NPRE = 13;
+    __device__ static void pack(const Pre &p, double (&f)[NPRE])
     {
+        f[0] = p.ru, f[1] = p.rv, f[2] = p.a00, f[3] = p.a01, f[4] = p.a10, f[5] = p.a11;
+        f[6] = p.det, f[7] = p.axu, f[8] = p.hax, f[9] = p.hay, f[10] = p.ayv, f[11] = p.u;
+        f[12] = p.v;
+    }
+    __device__ static Pre unpack(const double *f)
+    {
+        return Pre{f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8], f[9], f[10], f[11], f[12]};
+    }
+    __device__ static Pre pre(const Coeffs &cf, const Row &rw, const double *x, double invdx,
+                              double, bool)
+    {
+        Pre p;
         const double u = x[0], v = x[1];
         const double ax = cf.alpha * invdx, ay = rw.ay;
-        const double eu = (x[2] + e0) + n0;
-        const double ev = (x[3] + e1) + n1;
-        const double a00 = (1.0 + ax * u) + (0.5 * ay) * v;
-        const double a01 = (0.5 * ay) * u;
-        const double a10 = (0.5 * ax) * v;
-        const double a11 = (1.0 + ay * v) + (0.5 * ax) * u;
-        const double det = a00 * a11 - a01 * a10;
-        const double du = (a11 * eu - a01 * ev) / det;
-        const double dv = (a00 * ev - a10 * eu) / det;
-        const double m = v * du + u * dv;
-        e0 = (ax * u) * du;
-        e1 = (0.5 * ax) * m;
-        n0 = (0.5 * ay) * m;
-        n1 = (ay * v) * dv;
+        p.u = u;
+        p.v = v;
+        p.ru = x[2];
+        p.rv = x[3];
+        p.a00 = (1.0 + ax * u) + (0.5 * ay) * v;
+        p.a01 = (0.5 * ay) * u;
+        p.a10 = (0.5 * ax) * v;
+        p.a11 = (1.0 + ay * v) + (0.5 * ax) * u;
+        p.det = p.a00 * p.a11 - p.a01 * p.a10;
+        p.axu = ax * u;
+        p.hax = 0.5 * ax;
+        p.hay = 0.5 * ay;
+        p.ayv = ay * v;
+        return p;
+    }
+    template <bool FAST>
+    __device__ static void chain(const Pre &p, const Row &, double e0, double e1, double n0,
+                                 double n1, double &oe0, double &oe1, double &on0, double &on1,
+                                 double &o0, double &o1, bool &range_ok)
+    {
+        const double eu = (p.ru + e0) + n0;
+        const double ev = (p.rv + e1) + n1;
+        const double du = (p.a11 * eu - p.a01 * ev) / p.det;
+        const double dv = (p.a00 * ev - p.a10 * eu) / p.det;
+        const double m = p.v * du + p.u * dv;
+        oe0 = p.axu * du;
+        oe1 = p.hax * m;
+        on0 = p.hay * m;
+        on1 = p.ayv * dv;
         o0 = du;
         o1 = dv;
+        range_ok = true;
     }
     __device__ static void guess_e(const Coeffs &, const Io &, int, int, double &e0, double &e1)
     {
@@ -185,26 +289,257 @@ struct SolveCell {
 };
 
 // ---------------------------------------------------------------------------
-// One tile, one pass, one workgroup of kWaves wavefronts.  Wave 0 gathers the
-// inflow, decides whether the tile must be marched and sweeps it; all waves
-// stage the tile's inputs into LDS with coalesced row loads before the sweep
-// and write the outputs back coalesced after it (the sweeping wave touches
-// only LDS: lane l reads [l][s-l], conflict-free since the pitch TW-1 is odd).
-// Returns true (uniform over the workgroup) if the tile was marched.
-// Generation `cur` of the edge planes receives its outflow (marched or
-// carried), generation `prv` holds the neighbours' outflow of the previous
-// pass.
+// LDS image of one tile (one workgroup of kWaves wavefronts).
 constexpr int kWaves = 4;
 constexpr int kThreads = kWaves * kWave;
+constexpr int kEp = kWaves - 1;  // sweep steps per epoch: one diagonal per helper wave
+constexpr int kNE = 3;            // epochs held in the helper ring
+
+template <class C>
+constexpr int ring_pairs = (C::NPRE + 2 + 1) / 2;  // Pre fields + south inflow, as pairs
+
+template <class C, bool HELPED>
+struct Ring {
+    // [epoch][step][field pair][lane][2]: Pre fields, then the lane's south
+    // inflow (lane 0 only; +0.0 elsewhere); 16-byte pairs for b128 access
+    double v[kNE][kEp][ring_pairs<C>][kWave][2];
+};
+template <class C>
+struct Ring<C, false> {
+};
+
+// the helped sweep needs the tile (interleaved inputs) and the ring in LDS
+template <class C, int TW>
+constexpr bool helped_v = (size_t)C::NIN * TW * kWave * 8 +
+                              sizeof(double) * kNE * kEp * ring_pairs<C> * 2 * kWave <=
+                          150 * 1024;
 
 template <class C, int TW>
 struct TileLds {
-    double x[C::NIN][kWave * TW];  // staged inputs; planes 0/1 are overwritten by outputs
-    double dx[TW], src[TW];        // per-column inv_dx, src of the tile
-    double nout[2][TW];            // north outflow (top row), flushed after the sweep
+    Ring<C, helped_v<C, TW>> ring;  // first: every ring access has an immediate offset
+    double x[kWave * TW][C::NIN];   // inputs [row*TW + col][field]; fields 0/1 -> outputs
+    double dx[TW], src[TW];         // per-column inv_dx, src of the tile
+    double sedge[TW][2];            // south inflow of the tile
+    double nout[TW][2];             // north outflow (top row), flushed after the sweep
+    double trash[2][kWave][2];      // writes of lanes outside the tile this step
     int need;
 };
 
+// All waves: the tile's inputs, coalesced row segments -> LDS (missing cells
+// of a partial tile read as 1.0: harmless operands for the idle lanes).
+template <class C, int TW>
+__device__ void stage_tile(const Coeffs &cf, const typename C::Io &io, TileLds<C, TW> &sm,
+                           size_t tbase, int nrow, int ncol, int c0)
+{
+    const int tid = threadIdx.x;
+    const int nx = cf.nx;
+    constexpr int PER = kWave * TW / kThreads;  // elements per thread and plane
+    double v[C::NIN][PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {  // all loads in flight before any LDS store
+        const int e = tid + i * kThreads;
+        const int rr = e / TW, cc = e - rr * TW;
+        const bool ok = rr < nrow && cc < ncol;
+        const size_t g = tbase + (size_t)(ok ? rr : 0) * nx + (ok ? cc : 0);
+#pragma unroll
+        for (int q = 0; q < C::NIN; ++q) v[q][i] = ok ? io.in[q][g] : 1.0;
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i)
+#pragma unroll
+        for (int q = 0; q < C::NIN; ++q) sm.x[tid + i * kThreads][q] = v[q][i];
+    for (int cc = tid; cc < TW; cc += kThreads) {
+        const int c = c0 + min(cc, ncol - 1);
+        sm.dx[cc] = cf.inv_dx[c];
+        sm.src[cc] = cf.src[c];
+    }
+}
+
+// ---- generic sweep (one wave; SOLVE cell and 128-wide tiles): lane l
+// marches row r0+l, column j = s - l at step s.  Branch-free steps: every
+// lane evaluates a cell (idle lanes on clamped operands) and commits by
+// select.  Returns false if a FAST-sequence operand left its range.
+template <class C, int TW, bool FAST>
+__device__ bool sweep_tile(const Coeffs &cf, const Engine &eg, TileLds<C, TW> &sm, int t, int cur,
+                           int r, int nrow, int ncol, int c0, double we0, double we1)
+{
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool rowok = lane < nrow;
+    bool all_ok = true;
+    const typename C::Row rw = C::row(cf, r);
+    double e0 = we0, e1 = we1;    // running west inflow of my row
+    double no0 = 0.0, no1 = 0.0;  // my last north outflow (for lane + 1)
+    const int nsteps = ncol + nrow - 1;
+    const double(*xr)[C::NIN] = sm.x + lane * TW;
+    for (int s = 0; s < nsteps; ++s) {
+        const int jn = min(max(s - lane, 0), ncol - 1);
+        const typename C::Pre pc =
+            C::pre(cf, rw, xr[jn], sm.dx[jn], sm.src[jn], c0 + jn == 0);
+        const int sc = min(s, ncol - 1);
+        const double n0 = shr1(no0) + (lane == 0 ? sm.sedge[sc][0] : 0.0);
+        const double n1 = shr1(no1) + (lane == 0 ? sm.sedge[sc][1] : 0.0);
+        const int j = s - lane;
+        const bool act = rowok && j >= 0 && j < ncol;
+        double oe0, oe1, on0, on1, o0, o1;
+        bool ok;
+        C::template chain<FAST>(pc, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
+        all_ok = all_ok && (ok || !act);
+        e0 = act ? oe0 : e0;
+        e1 = act ? oe1 : e1;
+        no0 = on0;
+        no1 = on1;
+        double *d = act ? sm.x[lane * TW + j] : sm.trash[0][lane];
+        d[0] = o0;
+        d[1] = o1;
+        double *tn = act && lane == nrow - 1 ? sm.nout[j] : sm.trash[1][lane];
+        tn[0] = on0;
+        tn[1] = on1;
+    }
+    if (rowok) {
+        double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
+        ec[lane] = e0;
+        ec[kWave + lane] = e1;
+    }
+    return !__any(!all_ok);
+}
+
+// ---- helped sweep (all waves call it): wave 0 runs only the cell chains,
+// the DPP hand-over and its commits; waves 1..3 each precompute one diagonal
+// of every epoch into the ring, two epochs ahead of the sweep.
+template <class C, int TW, bool FAST>
+__device__ bool sweep_tile_helped(const Coeffs &cf, const Engine &eg, TileLds<C, TW> &sm, int t,
+                                  int cur, int r, int nrow, int ncol, int c0, double we0,
+                                  double we1)
+{
+    constexpr int NF = C::NPRE;
+    constexpr int NP = ring_pairs<C>;
+    const int wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & (kWave - 1);
+    const bool rowok = lane < nrow;
+    const int nsteps = ncol + nrow - 1;
+    const int nep = (nsteps + kEp - 1) / kEp;
+    const typename C::Row rw = C::row(cf, r);
+    // helper wave w (1..3) fills diagonal w-1 of epoch e
+    auto produce = [&](int e) {
+        const int i = wave - 1;
+        const int d = e * kEp + i;
+        const int jn = min(max(d - lane, 0), ncol - 1);
+        double f[2 * NP];
+        C::pack(C::pre(cf, rw, sm.x[lane * TW + jn], sm.dx[jn], sm.src[jn], c0 + jn == 0),
+                *reinterpret_cast<double(*)[NF]>(f));
+        const int sc = min(d, ncol - 1);
+        f[NF] = lane == 0 ? sm.sedge[sc][0] : 0.0;
+        f[NF + 1] = lane == 0 ? sm.sedge[sc][1] : 0.0;
+        if constexpr (2 * NP > NF + 2) f[2 * NP - 1] = 0.0;
+        double(*slot)[kWave][2] = sm.ring.v[e % kNE][i];
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+            slot[p][lane][0] = f[2 * p];
+            slot[p][lane][1] = f[2 * p + 1];
+        }
+    };
+    if (wave > 0) {
+        produce(0);
+        if (nep > 1) produce(1);
+    }
+    bool all_ok = true;
+    double e0 = we0, e1 = we1;    // running west inflow of my row
+    double no0 = 0.0, no1 = 0.0;  // my last north outflow (for lane + 1)
+    // a lane outside the tile rows never sees 0 <= j < ncol
+    const int jbase = rowok ? -lane : -(1 << 20);
+    double fc[2 * NP];  // ring fields of the current step
+#ifdef BURG_STAMPS
+    unsigned long long st0 = 0, wait_acc = 0;
+#endif
+    for (int b = 0; b < nep; ++b) {
+#ifdef BURG_STAMPS
+        const unsigned long long wa = __builtin_amdgcn_s_memtime();
+#endif
+        __syncthreads();  // epochs b, b+1 are in the ring; slot (b+2)%kNE is free
+#ifdef BURG_STAMPS
+        wait_acc += __builtin_amdgcn_s_memtime() - wa;
+#endif
+        if (wave == 0) {
+            const double(*cur_slots)[NP][kWave][2] = sm.ring.v[b % kNE];
+            const double(*nxt_slots)[NP][kWave][2] = sm.ring.v[(b + 1) % kNE];
+            if (b == 0) {
+#ifdef BURG_STAMPS
+                st0 = __builtin_amdgcn_s_memtime();
+#endif
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    fc[2 * p] = cur_slots[0][p][lane][0];
+                    fc[2 * p + 1] = cur_slots[0][p][lane][1];
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < kEp; ++i) {
+                const int s = b * kEp + i;
+                // next step's fields first (the next epoch's slot is ready)
+                double fn[2 * NP];
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    const double *src = i + 1 < kEp ? cur_slots[i + 1][p][lane]
+                                                    : nxt_slots[0][p][lane];
+                    fn[2 * p] = src[0];
+                    fn[2 * p + 1] = src[1];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                const typename C::Pre pc = C::unpack(fc);
+                // lane l takes the outflow of lane l-1; lane 0 gets +0.0 + its
+                // south inflow (exact: x + 0.0 == x)
+                const double n0 = shr1(no0) + fc[NF];
+                const double n1 = shr1(no1) + fc[NF + 1];
+                const int j = s + jbase;
+                const bool act = (unsigned)j < (unsigned)ncol;
+                double oe0, oe1, on0, on1, o0, o1;
+                bool ok;
+                C::template chain<FAST>(pc, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
+                all_ok = all_ok && (ok || !act);
+                e0 = act ? oe0 : e0;
+                e1 = act ? oe1 : e1;
+                no0 = on0;  // consumed by lane + 1 only when that lane is active,
+                no1 = on1;  // i.e. exactly when this lane was active last step
+                double *d = act ? sm.x[lane * TW + j] : sm.trash[0][lane];
+                d[0] = o0;
+                d[1] = o1;
+                double *tn = act && lane == nrow - 1 ? sm.nout[j] : sm.trash[1][lane];
+                tn[0] = on0;
+                tn[1] = on1;
+                // keep the next step's fields in registers (no re-read of LDS)
+#pragma unroll
+                for (int k = 0; k < 2 * NP; ++k) {
+                    asm volatile("" : "+v"(fn[k]));
+                    fc[k] = fn[k];
+                }
+            }
+        } else if (b + 2 < nep) {
+            produce(b + 2);
+        }
+    }
+    if (wave == 0) {
+#ifdef BURG_STAMPS
+        const unsigned long long st1 = __builtin_amdgcn_s_memtime();
+        if (lane == 0 && t == 0)
+            burg_stamp[0] = (long long)(st1 - st0), burg_stamp[1] = nsteps,
+            burg_stamp[2] = (long long)wait_acc;
+#endif
+        if (rowok) {
+            double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
+            ec[lane] = e0;
+            ec[kWave + lane] = e1;
+        }
+    }
+    return !__any(!all_ok);
+}
+
+// ---------------------------------------------------------------------------
+// One tile, one pass, one workgroup.  Wave 0 gathers the inflow and decides
+// whether the tile must be marched; all waves stage the tile into LDS and
+// write the outputs back coalesced.  Returns true (workgroup-uniform) if the
+// tile was marched.  Generation `cur` of the edge planes receives its outflow
+// (marched or carried), generation `prv` holds the neighbours' outflow of the
+// previous pass.
 template <class C, int TW>
 __device__ bool tile_pass(const Coeffs &cf, const Engine &eg, const typename C::Io &io, int t,
                           int pass, TileLds<C, TW> &sm)
@@ -292,21 +627,9 @@ __device__ bool tile_pass(const Coeffs &cf, const Engine &eg, const typename C::
         return false;
     }
 
-    // ---- stage the tile's inputs: coalesced row segments -> LDS [row][col]
+    // ---- stage the tile's inputs
     const size_t tbase = (size_t)r0 * nx + c0;
-    for (int e = tid; e < kWave * TW; e += kThreads) {
-        const int rr = e / TW, cc = e - rr * TW;
-        if (rr < nrow && cc < ncol) {
-            const size_t g = tbase + (size_t)rr * nx + cc;
-#pragma unroll
-            for (int q = 0; q < C::NIN; ++q) sm.x[q][e] = io.in[q][g];
-        }
-    }
-    for (int cc = tid; cc < TW; cc += kThreads) {
-        const int c = c0 + min(cc, ncol - 1);
-        sm.dx[cc] = cf.inv_dx[c];
-        sm.src[cc] = cf.src[c];
-    }
+    stage_tile<C, TW>(cf, io, sm, tbase, nrow, ncol, c0);
     if (wave == 0) {
         if (rowok) {
             wu[lane] = we0;
@@ -319,83 +642,35 @@ __device__ bool tile_pass(const Coeffs &cf, const Engine &eg, const typename C::
                 su[col] = sn0[q];
                 su[TW + col] = sn1[q];
             }
+            sm.sedge[col][0] = sn0[q];
+            sm.sedge[col][1] = sn1[q];
         }
     }
     __syncthreads();
 
-    // ---- wave 0: skewed sweep, lane l marches row r0+l, column j = s - l.
-    // Only LDS and registers inside the loop; the next step's operands are
-    // read one step ahead so the LDS latency hides under the cell's math.
-    if (wave == 0) {
-        const typename C::Row rw = C::row(cf, r);
-        double e0 = we0, e1 = we1;    // running west inflow of my row
-        double no0 = 0.0, no1 = 0.0;  // my last north outflow (for lane + 1)
-        const int nsteps = ncol + nrow - 1;
-        double *lrow[C::NIN];
-#pragma unroll
-        for (int q = 0; q < C::NIN; ++q) lrow[q] = sm.x[q] + lane * TW;
-        double xn[C::NIN], dxn, scn;
-        {
-            const int jn = min(max(-lane, 0), ncol - 1);
-#pragma unroll
-            for (int q = 0; q < C::NIN; ++q) xn[q] = lrow[q][jn];
-            dxn = sm.dx[jn];
-            scn = sm.src[jn];
-        }
-        for (int s = 0; s < nsteps; ++s) {
-            double xc[C::NIN];
-#pragma unroll
-            for (int q = 0; q < C::NIN; ++q) xc[q] = xn[q];
-            const double dxc = dxn, scc = scn;
-            {
-                const int jn = min(max(s + 1 - lane, 0), ncol - 1);
-#pragma unroll
-                for (int q = 0; q < C::NIN; ++q) xn[q] = lrow[q][jn];
-                dxn = sm.dx[jn];
-                scn = sm.src[jn];
-            }
-            double n0 = shr1(no0), n1 = shr1(no1);
-            if (s < ncol) {  // lane 0 takes the tile's south edge for column s
-                double a, b;
-                if constexpr (NQ == 1) {
-                    a = readlane(sn0[0], s);
-                    b = readlane(sn1[0], s);
-                } else {
-                    const int l = s & 63;
-                    a = (s >> 6) == 0 ? readlane(sn0[0], l) : readlane(sn0[NQ - 1], l);
-                    b = (s >> 6) == 0 ? readlane(sn1[0], l) : readlane(sn1[NQ - 1], l);
-                }
-                if (lane == 0) {
-                    n0 = a;
-                    n1 = b;
-                }
-            }
-            const int j = s - lane;
-            if (rowok && j >= 0 && j < ncol) {
-                double o0, o1;
-                C::cell(cf, rw, xc, dxc, scc, c0 + j, e0, e1, n0, n1, o0, o1);
-                lrow[0][j] = o0;
-                lrow[1][j] = o1;
-                no0 = n0;
-                no1 = n1;
-                if (lane == nrow - 1) {
-                    sm.nout[0][j] = n0;
-                    sm.nout[1][j] = n1;
-                }
-            }
-        }
-        if (rowok) {
-            double *ec = eg.eb[cur] + (size_t)t * 2 * kWave;
-            ec[lane] = e0;
-            ec[kWave + lane] = e1;
-        }
+    // ---- the sweep with the short exact sequences; if an operand left their
+    // range, restage and sweep again with the IEEE operators
+    bool ok = true;
+    if constexpr (helped_v<C, TW>) {
+        ok = sweep_tile_helped<C, TW, true>(cf, eg, sm, t, cur, r, nrow, ncol, c0, we0, we1);
+    } else {
+        if (wave == 0)
+            ok = sweep_tile<C, TW, true>(cf, eg, sm, t, cur, r, nrow, ncol, c0, we0, we1);
+    }
+    __syncthreads();
+    if (wave == 0 && lane == 0) sm.need = ok;
+    __syncthreads();
+    if (!sm.need) {
+        stage_tile<C, TW>(cf, io, sm, tbase, nrow, ncol, c0);
+        __syncthreads();
+        if (wave == 0) sweep_tile<C, TW, false>(cf, eg, sm, t, cur, r, nrow, ncol, c0, we0, we1);
     }
     __syncthreads();
     {
         double *nout = eg.nb[cur] + (size_t)t * 2 * TW;
         for (int cc = tid; cc < ncol; cc += kThreads) {
-            nout[cc] = sm.nout[0][cc];
-            nout[TW + cc] = sm.nout[1][cc];
+            nout[cc] = sm.nout[cc][0];
+            nout[TW + cc] = sm.nout[cc][1];
         }
     }
 
@@ -404,8 +679,8 @@ __device__ bool tile_pass(const Coeffs &cf, const Engine &eg, const typename C::
         const int rr = e / TW, cc = e - rr * TW;
         if (rr < nrow && cc < ncol) {
             const size_t g = tbase + (size_t)rr * nx + cc;
-            io.out[0][g] = sm.x[0][e];
-            io.out[1][g] = sm.x[1][e];
+            io.out[0][g] = sm.x[e][0];
+            io.out[1][g] = sm.x[e][1];
         }
     }
     __syncthreads();  // sm reused by the next tile
@@ -490,7 +765,6 @@ __global__ __launch_bounds__(kThreads) void final_kernel(Coeffs cf, Engine eg, t
         stats->passes += used;
         stats->tail_passes += tail;
         if (used > stats->max_passes) stats->max_passes = used;
-        // the engine keeps the generation parity of the final outflow
         *eg.ticket = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
@@ -506,14 +780,14 @@ int launch_pass(const Coeffs &cf, const Engine &eg, const typename C::Io &io, in
             final_kernel<C, 64><<<grid, block, 0, st>>>(cf, eg, io, pass, stats);
         else
             pass_kernel<C, 64><<<grid, block, 0, st>>>(cf, eg, io, pass);
-    } else if constexpr (C::NIN * 128 * kWave * 8 <= 160 * 1024) {
+    } else if constexpr (C::NIN * 128 * kWave * 8 <= 150 * 1024) {
         if (eg.tw != 128) return -1;
         if (final)
             final_kernel<C, 128><<<grid, block, 0, st>>>(cf, eg, io, pass, stats);
         else
             pass_kernel<C, 128><<<grid, block, 0, st>>>(cf, eg, io, pass);
     } else {
-        return -1;  // LDS budget: the 4-plane SOLVE cell needs tile_w = 64
+        return -1;  // LDS budget: the 4-input SOLVE cell needs tile_w = 64
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

@@ -225,8 +225,8 @@ int orc_newton_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
 /* Closed-form march (build's own exact solver; DESIGN.md section 3 "MARCH SPEC").
  * The implicit residual is lower-triangular in (r, c) and each cell's 2x2
  * system is u*s = Cu, v*s = Cv with the common factor s = 1 + hx u + hy v,
- * so s = 0.5 + sqrt(0.25 + hx Cu + hy Cv).  Op order is normative: the HIP
- * march reproduces it bit for bit.                                            */
+ * so s = 0.5 + sqrt(0.25 + hx Cu + hy Cv), u = Cu/s, v = Cv/s (IEEE sqrt and
+ * division).  Op order is normative: the HIP march reproduces it bit for bit. */
 void orc_march_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
                     const double *src, const double *lbc, double dt,
                     const double *wp, double *w)
@@ -259,8 +259,7 @@ void orc_march_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
             const double cv = (bv + yg[c]) + xhw;
             const double mm = fma(hx, cu, hy * cv);
             const double s = 0.5 + sqrt(0.25 + mm);
-            const double rs = 1.0 / s;
-            const double nu = cu * rs, nv = cv * rs;
+            const double nu = cu / s, nv = cv / s;
             const double hxu = hx * nu;
             xfw = fma(hxu, nu, xfp);
             xhw = fma(hxu, nv, xhp);
@@ -442,8 +441,7 @@ int orc_march_tiled_sim(int nx, int ny, const double *inv_dx, const double *inv_
                         const double cv = (bv + yg[c - c0]) + xhw;
                         const double mm = fma(hx, cu, hy * cv);
                         const double s = 0.5 + sqrt(0.25 + mm);
-                        const double rs = 1.0 / s;
-                        const double nu = cu * rs, nv = cv * rs;
+                        const double nu = cu / s, nv = cv / s;
                         const double hxu = hx * nu;
                         xfw = fma(hxu, nu, xfp);
                         xhw = fma(hxu, nv, xhp);
@@ -584,8 +582,7 @@ int orc_march_tiled_sim2(int nx, int ny, const double *inv_dx, const double *inv
                         const double cv = (bv + yg[c - c0]) + xhw;
                         const double mm = fma(hx, cu, hy * cv);
                         const double s = 0.5 + sqrt(0.25 + mm);
-                        const double rs = 1.0 / s;
-                        const double nu = cu * rs, nv = cv * rs;
+                        const double nu = cu / s, nv = cv / s;
                         const double hxu = hx * nu;
                         xfw = fma(hxu, nu, xfp);
                         xhw = fma(hxu, nv, xhp);

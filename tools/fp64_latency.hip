@@ -58,7 +58,8 @@ extern "C" __global__ void k_rsq(double *o, double a, double b, long long *t) {
 }
 // the march cell chain: inflow -> outflow, closed form with IEEE sqrt/div
 extern "C" __global__ void k_cell(double *o, double a, double b, long long *t) {
-    double e0 = o[threadIdx.x], e1 = 0.1, n0 = 0.2, n1 = 0.3;
+    double e0 = o[threadIdx.x & 63], e1 = 0.1, n0 = 0.2, n1 = 0.3;
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime();
     const double bu = 1.5, bv = 0.5, hx = 0.2, hy = 0.1, xfp = 0.3, xhp = 0.1, yhp = 0.05, ygp = 0.02;
     unsigned long long t0 = clk();
     for (int i = 0; i < N_IT; ++i) {
@@ -72,8 +73,9 @@ extern "C" __global__ void k_cell(double *o, double a, double b, long long *t) {
         n0 = fma(hy * nu, nv, yhp) * a; n1 = fma(hy * nv, nv, ygp) * a;
     }
     unsigned long long t1 = clk();
-    o[threadIdx.x] = e0 + e1 + n0 + n1;
-    if (threadIdx.x == 0) t[0] = (long long)(t1 - t0);
+    const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+    o[threadIdx.x & 63] = e0 + e1 + n0 + n1;
+    if (threadIdx.x == 0 && blockIdx.x == 0) { t[0] = (long long)(t1 - t0); t[1] = (long long)(r1 - r0); }
 }
 // same chain with hardware rcp/rsq + one Newton step each (not IEEE-exact)
 extern "C" __global__ void k_cell_fast(double *o, double a, double b, long long *t) {
@@ -100,7 +102,7 @@ extern "C" __global__ void k_cell_fast(double *o, double a, double b, long long 
 
 int main() {
     double *o; long long *t;
-    hipMalloc(&o, 64 * sizeof(double)); hipMalloc(&t, sizeof(long long));
+    hipMalloc(&o, 64 * sizeof(double)); hipMalloc(&t, 2 * sizeof(long long));
     double h[64]; for (int i = 0; i < 64; ++i) h[i] = 1.0 + i * 1e-3;
     struct { const char *n; void (*k)(double *, double, double, long long *); } ks[] = {
         {"fma dependent", k_fma}, {"fma x4 indep", k_fma4}, {"sqrt(+add)", k_sqrt},
@@ -115,6 +117,17 @@ int main() {
         long long c = 0; hipMemcpy(&c, t, sizeof c, hipMemcpyDeviceToHost);
         // s_memtime counts at the shader clock (MI355X_MICROARCH.md constants table)
         printf("%-26s %8.1f cycles/iter\n", k.n, (double)c / N_IT);
+    }
+    // in-kernel clock: s_memtime ticks / s_memrealtime (100 MHz) at 1 and 256 waves
+    for (int blocks : {1, 256, 1024}) {
+        for (int rep = 0; rep < 3; ++rep) {
+            hipMemcpy(o, h, sizeof h, hipMemcpyHostToDevice);
+            hipLaunchKernelGGL(k_cell, dim3(blocks), dim3(64), 0, 0, o, 0.999, 0.001, t);
+            hipDeviceSynchronize();
+        }
+        long long c[2] = {0, 0}; hipMemcpy(c, t, sizeof c, hipMemcpyDeviceToHost);
+        printf("cell chain, %4d waves: %8.1f ticks/iter, clock %.2f GHz\n", blocks,
+               (double)c[0] / N_IT, c[1] ? (double)c[0] / (c[1] * 10.0) : 0.0);
     }
     return 0;
 }
