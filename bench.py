@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nx", type=int, default=1024)
     ap.add_argument("--rows-per-gpu", type=int, default=None)
+    ap.add_argument("--engine", default="stream", choices=["stream", "tiles"])
+    ap.add_argument("--stream-w", type=int, default=0)
+    ap.add_argument("--tiles-target", type=int, default=0)
     ap.add_argument("--tile-w", type=int, default=64)
     ap.add_argument("--tol", type=float, default=2.0 ** -50)
     ap.add_argument("--profile-steps", type=int, default=10)
@@ -112,7 +115,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     ctx = make_slab_context(nx, ny, rank, world, device=local if world > 1 else 0,
-                            tile_w=args.tile_w, tol=args.tol)
+                            tile_w=args.tile_w, tol=args.tol, engine=args.engine,
+                            stream_w=args.stream_w, tiles_target=args.tiles_target)
     gx = np.linspace(0, 100, nx + 1)
     gy = np.linspace(0, 100.0 * ny / nx, ny + 1)  # same cell size: weak scaling
     ctx.set_problem(gx, gy, DT, MU, allow_nonsquare=(nx != ny))
@@ -150,9 +154,11 @@ def main():
             avg_ms = pst["march_kernel_ms"] / launches
             per_launch = alg_bytes / launches
             achieved = per_launch / (avg_ms * 1e-3) / 1e9
+            kname = (f"stream_kernel<{pst['stream_w']}>" if pst["engine"] == 0
+                     else f"march_pass_kernel<{args.tile_w}>")
             prof = dict(launches=launches, avg_ms=avg_ms, per_launch=per_launch,
                         achieved=achieved, passes=pst["passes"] / max(1, pst["steps"]),
-                        tile_marches=pst["tile_marches"])
+                        tile_marches=pst["tile_marches"], kernel=kname)
 
     if rank == 0:
         traffic, tsrc = read_pmc(args.pmc_file, nx, rows)
@@ -173,10 +179,12 @@ def main():
                 "workload": f"implicit 2D inviscid Burgers FOM, {nx}x{rows} cells per GPU "
                             f"(grid {nx}x{ny}), fp64, exact implicit step (HIP march)",
                 "nx": nx, "ny": ny, "rows_per_gpu": rows, "parallelism": f"row-slab x{world}",
-                "solver": "march", "tile_w": args.tile_w, "tol": args.tol,
+                "solver": "march", "engine": args.engine,
             },
-            "engine": {"passes_per_step": st["passes"] / max(1, st["steps"]),
-                       "max_passes": st["max_passes"],
+            "engine": {"name": args.engine, "stream_w": st["stream_w"],
+                       "tiles": st["stream_tiles"], "stall_spins": st["stall_spins"],
+                       "slow_diagonals": st["slow_diagonals"],
+                       "passes_per_step": st["passes"] / max(1, st["steps"]),
                        "unconverged_steps": st["unconverged_steps"],
                        "device_loop_ms": round(st["loop_ms"], 3)},
         }
@@ -185,7 +193,7 @@ def main():
                 "bound": "hbm", "achieved": round(prof["achieved"], 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(prof["achieved"] / HBM_PEAK_GBS, 5),
                 "traffic": traffic,
-                "kernel": "march_pass_kernel<64>",
+                "kernel": prof["kernel"],
                 "per_launch_alg_bytes": int(prof["per_launch"]),
                 "avg_launch_ms": round(prof["avg_ms"], 5),
                 "launches": prof["launches"],

@@ -13,18 +13,19 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_ERCCL = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
 SOLVERS = {"march": 0, "newton": 1}
+ENGINES = {"stream": 0, "tiles": 1}
 
 # Every symbol include/burgers.h declares (checked by tests/test_capi.py).
 EXPORTS = (
     "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_rccl_unique_id",
     "burg_ctx_create_slab", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
-    "burg_advance", "burg_download_state",
+    "burg_advance", "burg_download_state", "burg_set_engine",
 )
 
 
@@ -45,6 +46,12 @@ class BurgStats(ctypes.Structure):
         ("march_launches", ctypes.c_int64),
         ("last_rel", ctypes.c_double),
         ("tail_passes", ctypes.c_int64),
+        ("engine", ctypes.c_int32),
+        ("stream_w", ctypes.c_int32),
+        ("stream_tiles", ctypes.c_int64),
+        ("stall_spins", ctypes.c_int64),
+        ("slow_diagonals", ctypes.c_int64),
+        ("stream_launches", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -102,6 +109,7 @@ def load(path=None):
             "burg_advance": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(BurgStats)]),
             "burg_download_state": (ctypes.c_int, [_VP, _D]),
+            "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -58,6 +58,39 @@ struct DevStats {
     long long tail_passes;  // passes run by the final kernel's last workgroup
 };
 
+// ---- streaming engine (stream.hip) --------------------
+struct d2 {
+    double x, y;
+};
+
+struct StreamStats {
+    unsigned long long tile_steps;      // tile x step units marched
+    unsigned long long stall_spins;     // slow-path polls of not-yet-ready mailboxes
+    unsigned long long ieee_diagonals;  // diagonals re-run with IEEE sqrt/div (range)
+};
+
+// Tiling of a slab for the streaming engine: nti strips of 64 rows, ntj tiles
+// of W columns; R mailbox slots (steps) per edge.
+struct StreamPlan {
+    int W, nti, ntj, ntiles, R;
+};
+
+struct StreamArgs {
+    Coeffs cf;
+    const d2 *colc;      // [ntj*W] {hx, src} per column
+    d2 *ring;            // [ntiles][L][64] state by diagonal
+    d2 *wbox;            // [ntiles][R][64] west-edge mailboxes
+    d2 *sbox;            // [ntiles][R][W]  south-edge mailboxes
+    size_t wbox_bytes, sbox_bytes;
+    long long origin;    // ring entry of diagonal 0
+    long long L;         // ring length (diagonals)
+    int K;               // time steps of this launch
+    int flags;           // diagnostics only: bit 0 = ignore neighbours (wrong results)
+    int nti, ntj, ntiles, R;
+    unsigned *err;       // bit 0: a mailbox wait gave up
+    StreamStats *stats;
+};
+
 }  // namespace burg
 
 // ---- host-side launch wrappers (defined in the .hip files) ----------------
@@ -77,6 +110,15 @@ int residual_partials_count(const Coeffs &cf);
 int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y,
                hipStream_t st);
 int launch_axpy_neg(double *w, const double *d, size_t m, hipStream_t st);
+StreamPlan plan_stream(int nx, int ny, int tiles_target, int w_force);
+bool stream_width_supported(int W);
+int stream_max_resident_blocks(int W, int *per_cu, int *cus);
+int launch_stream(const StreamArgs &a, int W, hipStream_t st);
+int launch_colc(const Coeffs &cf, int ncols_pad, void *colc, hipStream_t st);
+int launch_fill_sentinel(void *p, size_t n16, hipStream_t st);
+int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st);
+int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
+                        int ldo, hipStream_t st);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
                      int ldo, hipStream_t st);
 

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -100,6 +101,16 @@ struct burg_ctx {
            *d_sumsq = nullptr;
     int npartials = 0;
     std::vector<hipEvent_t> prof_ev;
+
+    // streaming engine (stream.hip)
+    int engine = BURG_ENGINE_STREAM;
+    int stream_w_opt = 0, tiles_target_opt = 0;
+    StreamPlan sp{};
+    bool sp_ready = false, colc_ready = false;
+    d2 *d_colc = nullptr, *d_boxes = nullptr, *d_ring = nullptr;
+    size_t box16 = 0, ring_entries = 0;
+    unsigned *d_err = nullptr;
+    StreamStats *d_sstats = nullptr;
 
     size_t m() const { return 2 * (size_t)nx * nrows; }
     size_t n() const { return (size_t)nx * nrows; }
@@ -265,8 +276,305 @@ int read_stats(burg_ctx *c, burg_stats *st)
         st->unconverged_steps = ds.unconverged_steps;
         st->tail_passes = ds.tail_passes;
         st->par_passes = c->par_passes;
+        st->engine = BURG_ENGINE_TILES;
     }
     return 0;
+}
+
+// ---- streaming engine -------------------------------------------------------
+void stream_free(burg_ctx *c)
+{
+    dfree(c->d_colc);
+    dfree(c->d_boxes);
+    dfree(c->d_ring);
+    dfree(c->d_err);
+    dfree(c->d_sstats);
+    c->ring_entries = 0;
+    c->sp_ready = c->colc_ready = false;
+}
+
+// Plan the tiling (capped by residency: every tile's wavefront must be live
+// at once), allocate the mailboxes (all sentinel) and the column table.
+int stream_setup(burg_ctx *c)
+{
+    if (!c->sp_ready) {
+        const int target = c->tiles_target_opt > 0 ? c->tiles_target_opt : 1024;
+        StreamPlan p = plan_stream(c->nx, c->nrows, target, c->stream_w_opt);
+        for (;;) {
+            if (!stream_width_supported(p.W))
+                return fail(BURG_EINVAL, "stream tile width %d not supported (8..4096, power of 2)",
+                            p.W);
+            int per_cu = 0, cus = 0;
+            const int cap = stream_max_resident_blocks(p.W, &per_cu, &cus);
+            if (cap < 0) return fail(BURG_EHIP, "occupancy query failed");
+            if (p.ntiles <= 4 * cap) break;
+            if (c->stream_w_opt > 0 || p.W >= 4096)
+                return fail(BURG_ESHAPE, "%d tiles of width %d exceed the %d resident wavefronts",
+                            p.ntiles, p.W, 4 * cap);
+            p = plan_stream(c->nx, c->nrows, 0, p.W * 2);
+        }
+        c->sp = p;
+        c->box16 = (size_t)p.ntiles * p.R * (kWave + p.W);
+        if (int e = dalloc(&c->d_boxes, c->box16)) return e;
+        if (int e = dalloc(&c->d_colc, (size_t)p.ntj * p.W)) return e;
+        if (int e = dalloc(&c->d_err, 4)) return e;
+        if (int e = dalloc(&c->d_sstats, 1)) return e;
+        CHK(launch_fill_sentinel(c->d_boxes, c->box16, c->stream));
+        HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
+        c->sp_ready = true;
+        c->colc_ready = false;
+    }
+    if (!c->colc_ready) {
+        CHK(launch_colc(c->cf, c->sp.ntj * c->sp.W, c->d_colc, c->stream));
+        c->colc_ready = true;
+    }
+    return 0;
+}
+
+int ensure_ring(burg_ctx *c, long long L)
+{
+    const size_t need = (size_t)c->sp.ntiles * (size_t)L * kWave;
+    if (need <= c->ring_entries) return 0;
+    dfree(c->d_ring);
+    c->ring_entries = 0;
+    if (int e = dalloc(&c->d_ring, need)) return e;
+    c->ring_entries = need;
+    return 0;
+}
+
+StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
+{
+    StreamArgs a{};
+    a.cf = c->cf;
+    a.colc = c->d_colc;
+    a.ring = c->d_ring;
+    a.wbox = c->d_boxes;
+    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * c->sp.R * kWave;
+    a.wbox_bytes = (size_t)c->sp.ntiles * c->sp.R * kWave * sizeof(d2);
+    a.sbox_bytes = (size_t)c->sp.ntiles * c->sp.R * c->sp.W * sizeof(d2);
+    a.origin = origin;
+    a.L = L;
+    a.K = K;
+    a.nti = c->sp.nti;
+    a.ntj = c->sp.ntj;
+    a.ntiles = c->sp.ntiles;
+    a.R = c->sp.R;
+    a.err = c->d_err;
+    a.stats = c->d_sstats;
+    if (const char *e = std::getenv("BURG_STREAM_DEBUG")) a.flags = std::atoi(e);  // diagnostics
+    return a;
+}
+
+// max steps per launch so that K*W stays an int
+int stream_max_steps(const burg_ctx *c) { return (1 << 29) / c->sp.W; }
+
+int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
+{
+    const StreamArgs a = stream_args(c, L, origin, K);
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    CHK(launch_stream(a, c->sp.W, c->stream));
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    float t = 0.f;
+    HIPCHK(hipEventElapsedTime(&t, c->ev0, c->ev1));
+    *ms += t;
+    unsigned err[4] = {0, 0, 0, 0};
+    HIPCHK(hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
+    if (err[0]) {
+        // leave the mailboxes clean for the next launch
+        (void)hipMemsetAsync(c->d_err, 0, sizeof err, c->stream);
+        (void)launch_fill_sentinel(c->d_boxes, c->box16, c->stream);
+        (void)hipStreamSynchronize(c->stream);
+        return fail(BURG_EHIP,
+                    "streaming engine: an edge wait timed out (tile %u of %d, diagonal %u, "
+                    "edges %u [1 west 2 south 4 east 8 north], K=%d W=%d)",
+                    err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W);
+    }
+    return 0;
+}
+
+void stream_stats_begin(burg_ctx *c)
+{
+    (void)hipMemsetAsync(c->d_sstats, 0, sizeof(StreamStats), c->stream);
+}
+
+int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launches)
+{
+    StreamStats ss{};
+    HIPCHK(hipMemcpyAsync(&ss, c->d_sstats, sizeof ss, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (st) {
+        st->steps = steps;
+        st->tile_marches = (int64_t)ss.tile_steps;
+        st->passes = steps;
+        st->max_passes = steps > 0 ? 1 : 0;
+        st->unconverged_steps = 0;
+        st->engine = BURG_ENGINE_STREAM;
+        st->stream_w = c->sp.W;
+        st->stream_tiles = c->sp.ntiles;
+        st->stall_spins = (int64_t)ss.stall_spins;
+        st->slow_diagonals = (int64_t)ss.ieee_diagonals;
+        st->stream_launches = launches;
+    }
+    return 0;
+}
+
+// advance the device state d_state[cur] by num_steps with the streaming engine
+int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
+{
+    if (int e = stream_setup(c)) return e;
+    const int W = c->sp.W;
+    const long long L = 2LL * W + 32;
+    if (int e = ensure_ring(c, L)) return e;
+    stream_stats_begin(c);
+    CHK(launch_ring_load(stream_args(c, L, 0, 0), W, c->d_state[c->cur], c->stream));
+    float ms = 0.f;
+    long long origin = 0;
+    int done = 0, last = 0;
+    int64_t launches = 0;
+    while (done < num_steps) {
+        const int K = std::min(num_steps - done, stream_max_steps(c));
+        if (int e = stream_launch(c, L, origin, K, &ms)) return e;
+        origin = (origin + (long long)K * W) % L;
+        done += K;
+        last = K;
+        ++launches;
+    }
+    if (num_steps > 0) {
+        // the final state is state `last` of the last launch (origin before it)
+        const long long o_last = ((origin - (long long)last * W) % L + L) % L;
+        CHK(launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1,
+                                c->d_state[c->cur ^ 1], 1, c->stream));
+        c->cur ^= 1;
+    }
+    if (int e = stream_stats_end(c, st, num_steps, launches)) return e;
+    if (st) {
+        st->loop_ms = ms;
+        if (c->profile) {
+            st->march_kernel_ms = ms;
+            st->march_launches = launches;
+        }
+    }
+    return 0;
+}
+
+// burg_run for the march solver on the streaming engine: the ring holds a
+// chunk of C steps; after each chunk the snapshot columns it covers are
+// transposed into the host matrix.
+int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int64_t ld_snaps,
+               int snap_every, burg_stats *st, int32_t *step_iters, double *step_rel)
+{
+    if (int e = stream_setup(c)) return e;
+    const int W = c->sp.W;
+    const size_t m = c->m(), bytes = m * sizeof(double);
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    // ring: up to a third of free memory (a step of ring = one state)
+    long long Lmax = (long long)(freeb / 3 / per_entry);
+    long long C = (Lmax - W - 96) / W;
+    C = std::min<long long>(C, std::max(num_steps, 1));
+    C = std::min<long long>(C, stream_max_steps(c));
+    if (const char *e = std::getenv("BURG_STREAM_CHUNK")) {  // test knob: force chunking
+        const long long v = std::atoll(e);
+        if (v > 0) C = std::min(C, v);
+    }
+    if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
+    const long long L = C * W + W + 96;
+    dfree(c->d_ring);
+    c->ring_entries = 0;
+    if (int e = ensure_ring(c, L)) return e;
+
+    // snapshot staging: S columns at a time
+    int S = 0;
+    double *d_tr = nullptr;
+    bool registered = false;
+    const int64_t ncols = num_steps / snap_every + 1;
+    if (snaps) {
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        S = (int)std::min<int64_t>(ncols, 64);
+        while (S > 1 && (size_t)S * bytes > freeb / 3) S /= 2;
+        if (int e = dalloc(&d_tr, (size_t)S * m)) return e;
+        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
+                                     hipHostRegisterDefault) == hipSuccess;
+        (void)hipGetLastError();
+    }
+    float flush_ms = 0.f;
+    hipEvent_t f0 = nullptr, f1 = nullptr;
+    (void)hipEventCreate(&f0);
+    (void)hipEventCreate(&f1);
+    // copy host columns [col, col+cnt) = states k0 + j*snap_every (relative to origin)
+    auto flush = [&](long long origin, int k0, int cnt, int64_t col) -> int {
+        for (int j0 = 0; j0 < cnt; j0 += S) {
+            const int n = std::min(S, cnt - j0);
+            HIPCHK(hipEventRecord(f0, c->stream));
+            CHK(launch_ring_extract(stream_args(c, L, origin, 0), W, k0 + j0 * snap_every,
+                                    snap_every, n, d_tr, n, c->stream));
+            HIPCHK(hipMemcpy2DAsync(snaps + col + j0, (size_t)ld_snaps * sizeof(double), d_tr,
+                                    n * sizeof(double), n * sizeof(double), m,
+                                    hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipEventRecord(f1, c->stream));
+            HIPCHK(hipEventSynchronize(f1));
+            float t = 0.f;
+            (void)hipEventElapsedTime(&t, f0, f1);
+            flush_ms += t;
+        }
+        return 0;
+    };
+
+    int rc = BURG_OK;
+    stream_stats_begin(c);
+    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, bytes, hipMemcpyHostToDevice, c->stream));
+    CHK(launch_ring_load(stream_args(c, L, 0, 0), W, c->d_state[c->cur], c->stream));
+    if (snaps) rc = flush(0, 0, 1, 0);
+    float ms = 0.f;
+    long long origin = 0;
+    int done = 0, last = 0;
+    int64_t launches = 0;
+    while (rc == BURG_OK && done < num_steps) {
+        const int K = (int)std::min<long long>(num_steps - done, C);
+        rc = stream_launch(c, L, origin, K, &ms);
+        if (rc) break;
+        ++launches;
+        if (snaps) {
+            // columns j with done < j*snap_every <= done + K
+            const int64_t j0 = done / snap_every + 1, j1 = (done + K) / snap_every;
+            if (j1 >= j0)
+                rc = flush(origin, (int)(j0 * snap_every - done), (int)(j1 - j0 + 1), j0);
+        }
+        origin = (origin + (long long)K * W) % L;
+        done += K;
+        last = K;
+    }
+    if (rc == BURG_OK && num_steps > 0) {
+        const long long o_last = ((origin - (long long)last * W) % L + L) % L;
+        rc = launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1,
+                                 c->d_state[c->cur ^ 1], 1, c->stream);
+        if (rc == -3) rc = fail(BURG_EHIP, "ring extract launch failed");
+        else c->cur ^= 1;
+    }
+    if (rc == BURG_OK) rc = stream_stats_end(c, st, num_steps, launches);
+    if (st) {
+        st->loop_ms = ms;
+        st->flush_ms = flush_ms;
+        if (c->profile) {
+            st->march_kernel_ms = ms;
+            st->march_launches = launches;
+        }
+    }
+    for (int s = 0; s < num_steps; ++s) {
+        if (step_iters) step_iters[s] = 1;
+        if (step_rel) step_rel[s] = 0.0;
+    }
+    (void)hipStreamSynchronize(c->stream);
+    if (registered) (void)hipHostUnregister(snaps);
+    dfree(d_tr);
+    // the ring of a long run can be large: give it back
+    dfree(c->d_ring);
+    c->ring_entries = 0;
+    (void)hipEventDestroy(f0);
+    (void)hipEventDestroy(f1);
+    return rc;
 }
 
 }  // namespace
@@ -354,6 +662,7 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_x);
     dfree(c->d_partials);
     dfree(c->d_sumsq);
+    stream_free(c);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -391,6 +700,7 @@ int burg_set_problem(burg_ctx *c, const double *inv_dx, const double *inv_dy,
     c->cf.nx = c->nx;
     c->cf.ny = c->nrows;
     c->have_problem = true;
+    c->colc_ready = false;
     return BURG_OK;
 }
 
@@ -406,6 +716,25 @@ int burg_set_options(burg_ctx *c, int tile_w, int par_passes, double tol, int pr
     c->tol = tol;
     c->profile = profile ? 1 : 0;
     return engine_alloc(c);
+}
+
+int burg_set_engine(burg_ctx *c, int engine, int stream_w, int tiles_target)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (engine != BURG_ENGINE_STREAM && engine != BURG_ENGINE_TILES)
+        return fail(BURG_EINVAL, "unknown engine %d", engine);
+    if (stream_w != 0 && !stream_width_supported(stream_w))
+        return fail(BURG_EINVAL, "stream_w must be 0 or a power of two in [8, 4096]");
+    if (tiles_target < 0) return fail(BURG_EINVAL, "tiles_target < 0");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->engine = engine;
+    if (stream_w != c->stream_w_opt || tiles_target != c->tiles_target_opt) {
+        stream_free(c);
+        c->stream_w_opt = stream_w;
+        c->tiles_target_opt = tiles_target;
+    }
+    return BURG_OK;
 }
 
 int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, double *norm)
@@ -479,6 +808,8 @@ int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
     if (solver != BURG_SOLVER_MARCH && solver != BURG_SOLVER_NEWTON)
         return fail(BURG_EINVAL, "unknown solver %d", solver);
     if (st) std::memset(st, 0, sizeof *st);
+    if (solver == BURG_SOLVER_MARCH && c->engine == BURG_ENGINE_STREAM)
+        return stream_advance(c, num_steps, st);
     HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream));
     if (solver == BURG_SOLVER_NEWTON)
         if (int e = ensure_scratch(c)) return e;
@@ -531,6 +862,9 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
                     (long long)ncols);
     if (newton_max_its < 0) return fail(BURG_EINVAL, "newton_max_its < 0");
     if (st) std::memset(st, 0, sizeof *st);
+    if (solver == BURG_SOLVER_MARCH && c->engine == BURG_ENGINE_STREAM)
+        return stream_run(c, w0, num_steps, snaps, ld_snaps, snap_every, st, step_iters,
+                          step_rel);
     if (int e = ensure_scratch(c)) return e;
     const size_t m = c->m(), bytes = m * sizeof(double);
 

@@ -1,0 +1,515 @@
+// stream.hip -- the streaming engine: K implicit time steps of the 2D inviscid
+// Burgers FOM in ONE launch, exactly the sequential march (orc_march_step,
+// bit for bit), pipelined over tiles and time steps.
+//
+// Why this works: the reference residual (C/hypernet2D.py:2512-2570) couples
+// a cell only to itself and its west/south neighbours, so the implicit step
+// is a forward substitution in (row, column) order (cell_math.h), and step
+// n+1 of a cell needs only step n of the same cell.  The dependence graph over
+// (step, row, column) is therefore a 3-D wavefront with no iteration at all.
+//
+// Mapping: a tile = 64 rows (one per lane) x W columns, owned by ONE wavefront
+// for the whole launch.  At diagonal s lane r works on local time t = s - r,
+// i.e. step t / W + 1, column t % W: lane r+1 trails lane r by one diagonal, so
+// the south inflow of every lane is its neighbour's north outflow of the
+// previous diagonal (one DPP move), and the west inflow is the lane's own east
+// outflow of the previous diagonal.  The skew runs continuously across time
+// steps, so after a 63-diagonal ramp every lane does useful work every
+// diagonal.
+//
+// State lives in a per-tile ring indexed by diagonal: entry s holds, for every
+// lane r, the state that lane produced at diagonal s.  The previous step of the
+// same cell was produced exactly W diagonals earlier by the same lane, so the
+// read for diagonal s is entry s - W: both the read and the write of a
+// diagonal are one contiguous 1 KB row (64 lanes x {u, v}), fully coalesced.
+//
+// Between tiles: outflows cross tile edges through mailboxes of 16-byte
+// granules (west edge: 64 rows, south edge: W columns, R step slots each).
+// A granule is data-as-flag: the producer writes it write-through (sc1), the
+// consumer polls it with sc1 loads until neither half is the sentinel, uses
+// it, and writes the sentinel back; the producer checks the slot holds the
+// sentinel before reusing it R steps later.  No fences, no counters
+// (MI355X_MICROARCH.md, hand-off forms R2).  Every wait is bounded: a wave that
+// gives up sets the error word and the launch still drains.
+#include "burg_internal.h"
+#include "cell_math.h"
+
+namespace burg {
+namespace {
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+constexpr unsigned long long kSentBits = 0x7FF4DEADBEEF5A5AULL;  // a signalling NaN:
+                                                                  // never produced by arithmetic
+constexpr int kSpinLimit = 1 << 21;  // ~seconds: only a broken pipeline gets there
+
+constexpr unsigned kSentHi = (unsigned)(kSentBits >> 32);
+constexpr unsigned kOOB = 0xC0000000u;  // past every mailbox descriptor's range, also
+                                        // after adding a slot offset (< 2^30)
+
+// A granule is {x, y} as two little-endian doubles: the high words (where the
+// sentinel test looks) are dwords 1 and 3.
+__device__ __forceinline__ d2 as_d2(v4u v)
+{
+    d2 r;
+    r.x = __hiloint2double((int)v.y, (int)v.x);
+    r.y = __hiloint2double((int)v.w, (int)v.z);
+    return r;
+}
+
+__device__ __forceinline__ v4u as_v4u(double a, double b)
+{
+    v4u v;
+    v.x = (unsigned)__double2loint(a);
+    v.y = (unsigned)__double2hiint(a);
+    v.z = (unsigned)__double2loint(b);
+    v.w = (unsigned)__double2hiint(b);
+    return v;
+}
+
+__device__ __forceinline__ bool has_sent(v4u g) { return g.y == kSentHi || g.w == kSentHi; }
+__device__ __forceinline__ bool all_sent(v4u g) { return g.y == kSentHi && g.w == kSentHi; }
+
+// lane i <- lane i-1; lane 0 keeps `old0` (its own value of `old0`)
+__device__ __forceinline__ double shr1_or(double old0, double x)
+{
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old0), __double2loint(x), 0x138,
+                                               0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old0), __double2hiint(x), 0x138,
+                                               0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ v4u ld_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
+}
+
+__device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+}
+
+template <int W>
+constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
+
+// One wavefront per tile; 4 tiles per workgroup (one per SIMD).
+template <int W, int D>
+__global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
+{
+    static_assert((W & (W - 1)) == 0 && W > D, "W: power of two > D");
+    constexpr int LW = ilog2<W>();
+    const int lane = threadIdx.x & (kWave - 1);
+    const int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    if (tile >= a.ntiles) return;
+    const int ti = tile / a.ntj, tj = tile - ti * a.ntj;
+    const int ny = a.cf.ny;
+    const int nrow = min(kWave, ny - ti * kWave);
+    const int top = nrow - 1;
+    const bool iso = a.flags & 1;
+    const bool has_west = tj > 0 && !iso, has_east = tj + 1 < a.ntj && !iso;
+    const bool has_south = ti > 0 && !iso, has_north = ti + 1 < a.nti && !iso;
+    const bool rowok = lane < nrow;
+    const int Rm = a.R - 1;
+    const int KW = a.K * W;
+
+    // row coefficients (MarchCell::row); padding lanes reuse the top row
+    const int r = ti * kWave + min(lane, top);
+    const double ay = a.cf.alpha * a.cf.inv_dy[r];
+    const double hy = 0.5 * ay;
+    const double lb = a.cf.lbc[r];
+    const bool col0_tile = tj == 0;
+
+    const d2 *__restrict__ colc = a.colc + (size_t)tj * W;
+    const d2 *ringt = a.ring + (size_t)tile * a.L * kWave;
+    d2 *ringw = a.ring + (size_t)tile * a.L * kWave;
+    const __amdgpu_buffer_rsrc_t wbox =
+        __builtin_amdgcn_make_buffer_rsrc(a.wbox, 0, (int)a.wbox_bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t sbox =
+        __builtin_amdgcn_make_buffer_rsrc(a.sbox, 0, (int)a.sbox_bytes, 0x00020000);
+    // mailbox byte offsets: west box of tile t, slot q, row l: ((t*R + q)*64 + l)*16;
+    // south box of tile t, slot q, column c: ((t*R + q)*W + c)*16
+    const unsigned wb_mine = (unsigned)tile * a.R * kWave * 16u + lane * 16u;
+    const unsigned wb_step = (unsigned)a.R * kWave * 16u;  // -> the east tile's box
+    const unsigned sb_mine = (unsigned)tile * a.R * W * 16u;
+    const unsigned sb_step = (unsigned)a.ntj * a.R * W * 16u;  // -> the north tile's box
+    const v4u sent = as_v4u(__longlong_as_double((long long)kSentBits),
+                            __longlong_as_double((long long)kSentBits));
+
+    // ring positions (diagonal -> entry), wave-uniform
+    const long long L = a.L;
+    long long pw = a.origin;                         // entry of diagonal s
+    long long pr = ((a.origin - W) % L + L) % L;    // entry read by the next prefetch
+                                                     // (diagonal sp - W for sp = 0, 1, ...)
+
+    // Per slot i (diagonal s = i mod D), prefetched D diagonals ahead:
+    //   gw: the lane's west/east granule -- at column 0 the west inflow of this
+    //       step (consume), at column W-1 the east tile's slot (must be empty)
+    //   gs: lane 0: the south inflow granule; lane `top`: the north tile's slot
+    //   ow, os: the byte offsets of gw, gs (kOOB where the lane has no access:
+    //       buffer loads there return 0 and stores are dropped)
+    // and, for wide tiles (!REG), pf: the lane's state of the previous step
+    // (ring entry s - W) and cc: {hx, src} of the lane's column.
+    // Narrow tiles (REG, W <= 16) keep both in registers instead: the lane's
+    // previous-step state of diagonal s is its own output of diagonal s - W,
+    // i.e. the same unrolled slot one round earlier, and its column at slot i
+    // is (i - lane) mod W every round.
+    constexpr bool REG = W <= 16;
+    constexpr int U = REG ? W : D;  // unroll (diagonals per round)
+    static_assert(U % D == 0, "prefetch slots must tile the unroll");
+    v4u gw[D], gs[D];
+    unsigned ow[D], os[D];
+    d2 pf[REG ? 1 : D], cc[REG ? 1 : D];
+    d2 st[REG ? W : 1], ccr[REG ? W : 1];
+    const int lane_j = lane;  // keep lane in a VGPR
+    // bases with the tile's neighbourhood folded in (kOOB: no such neighbour).
+    // Padding lanes (rows past the grid in a partial strip) stay out of the
+    // edge protocol: their consumer would not wait (only real rows take the
+    // slow path), so it could empty a slot before the producer filled it.
+    const unsigned wcb = has_west && rowok ? wb_mine : kOOB;            // west inflow
+    const unsigned wpb = has_east && rowok ? wb_mine + wb_step : kOOB;  // east outflow
+    // lane 0 consumes the south edge, lane `top` produces the north edge
+    const unsigned slb = lane == 0 ? (has_south ? sb_mine : kOOB)
+                                   : (lane == top && has_north ? sb_mine + sb_step : kOOB);
+    auto prefetch = [&](int sp, int i) {
+        const int tp = sp - lane_j;
+        const int cp = tp & (W - 1);
+        const unsigned qp = (unsigned)(tp >> LW) & (unsigned)Rm;
+        const bool vp = (unsigned)tp < (unsigned)KW;
+        if constexpr (!REG) {
+            pf[i] = ringt[(size_t)pr * kWave + lane];
+            cc[i] = colc[cp];
+            pr = pr + 1 == L ? 0 : pr + 1;
+        }
+        const unsigned o = cp == 0 ? wcb : (cp == W - 1 ? wpb : kOOB);
+        ow[i] = vp ? o + (qp << 10) : kOOB;
+        gw[i] = ld_sc1(wbox, ow[i]);
+        os[i] = vp ? slb + ((qp << LW) | (unsigned)cp) * 16u : kOOB;
+        gs[i] = ld_sc1(sbox, os[i]);
+    };
+
+    if constexpr (REG) {
+        // state 0 of column (i - lane) mod W sits at diagonal c + lane - W
+#pragma unroll
+        for (int i = 0; i < W; ++i) {
+            const int c = (i - lane_j) & (W - 1);
+            long long e = (a.origin + c + lane_j - W) % L;
+            e = e < 0 ? e + L : e;
+            st[i] = ringt[(size_t)e * kWave + lane];
+            ccr[i] = colc[c];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) prefetch(i, i);
+
+    double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
+    unsigned spins = 0;
+    bool bad_range = false;
+
+    // one diagonal: slot k of the prefetch ring, u of the unroll
+    auto diagonal = [&](const int s, const int u, const bool ramp) {
+        const int k = u % D;
+        const int t = s - lane_j;
+        const int c = t & (W - 1);
+        const bool valid = (unsigned)t < (unsigned)KW;
+        const bool at0 = c == 0, atE = c == W - 1;
+        const bool s_in = lane == 0, n_out = lane == top && lane != 0;
+        // ---- the cell (MarchCell::pre + chain, same op order)
+        const d2 x = REG ? st[u % (REG ? W : 1)] : pf[k % (REG ? 1 : D)];
+        const d2 co = REG ? ccr[u % (REG ? W : 1)] : cc[k % (REG ? 1 : D)];
+        const double pu = x.x, pv = x.y;
+        const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
+        const double sl = (col0_tile && at0) ? co.y + lb : co.y;
+        MarchCell::Pre p;
+        p.hx = hx;
+        const double hu = 0.5 * pu;
+        p.xfp = ax * (hu * pu);
+        p.xhp = ax * (hu * pv);
+        p.yhp = ay * (hu * pv);
+        p.ygp = ay * ((0.5 * pv) * pv);
+        p.bu = ((pu - p.xfp) - p.yhp) + sl;
+        p.bv = (pv - p.ygp) - p.xhp;
+        const MarchCell::Row rw{ay, hy, lb};
+        // producers: the east / north slot must be empty (sentinel in both halves)
+        bool pbad = false;
+        if (has_east) pbad |= valid && rowok && atE && !all_sent(gw[k]);
+        if (has_north) pbad |= valid && n_out && !all_sent(gs[k]);
+        // west inflow at column 0: the granule, or +0.0 at the domain
+        // boundary (the load was out of range); south inflow of lane 0 likewise.
+        // A granule not yet written holds the sentinel NaN, which fails the
+        // chain's range check: the slow path below then waits for it.
+        if (at0) {
+            const d2 g = as_d2(gw[k]);
+            e0 = g.x;
+            e1 = g.y;
+        }
+        double n0 = shr1_or(as_d2(gs[k]).x, no0);
+        double n1 = shr1_or(as_d2(gs[k]).y, no1);
+        double oe0, oe1, on0, on1, o0, o1;
+        bool ok;
+        MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
+        if (__builtin_expect(__any((!ok && valid && rowok) || pbad), 0)) {
+            // slow path: poll the granules until inputs are written and
+            // output slots are free, then redo the cell with IEEE sqrt/div
+            for (;;) {
+                gw[k] = ld_sc1(wbox, ow[k]);
+                gs[k] = ld_sc1(sbox, os[k]);
+                bool b = false;
+                if (has_west) b |= valid && rowok && at0 && has_sent(gw[k]);
+                if (has_south) b |= valid && s_in && has_sent(gs[k]);
+                if (has_east) b |= valid && rowok && atE && !all_sent(gw[k]);
+                if (has_north) b |= valid && n_out && !all_sent(gs[k]);
+                if (!__any(b)) break;
+                if (++spins >= kSpinLimit) {
+                    // report which wait gave up: tile, diagonal, and which edge
+                    unsigned why = 0;
+                    if (has_west && __any(valid && rowok && at0 && has_sent(gw[k]))) why |= 1;
+                    if (has_south && __any(valid && s_in && has_sent(gs[k]))) why |= 2;
+                    if (has_east && __any(valid && rowok && atE && !all_sent(gw[k]))) why |= 4;
+                    if (has_north && __any(valid && n_out && !all_sent(gs[k]))) why |= 8;
+                    if (lane == 0 && atomicOr(a.err, 1u) == 0) {
+                        a.err[1] = tile;
+                        a.err[2] = s;
+                        a.err[3] = why;
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+            if (at0) {
+                const d2 g = as_d2(gw[k]);
+                e0 = g.x;
+                e1 = g.y;
+            }
+            n0 = shr1_or(as_d2(gs[k]).x, no0);
+            n1 = shr1_or(as_d2(gs[k]).y, no1);
+            MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
+            bad_range = true;
+        }
+        e0 = oe0;
+        e1 = oe1;
+        no0 = on0;
+        no1 = on1;
+        // ---- outputs
+        if constexpr (REG) {
+            // lanes that have not started keep their step-0 state
+            if (ramp) {
+                if (t >= 0) st[u % (REG ? W : 1)] = d2{o0, o1};
+            } else {
+                st[u % (REG ? W : 1)] = d2{o0, o1};
+            }
+        }
+        if (valid) ringw[(size_t)pw * kWave + lane] = d2{o0, o1};
+        st_sc1(wbox, at0 ? ow[k] : kOOB, sent);                  // consumed: empty it
+        st_sc1(wbox, atE ? ow[k] : kOOB, as_v4u(oe0, oe1));      // east outflow
+        st_sc1(sbox, s_in ? os[k] : kOOB, sent);
+        st_sc1(sbox, s_in ? kOOB : os[k], as_v4u(on0, on1));     // north outflow
+        pw = pw + 1 == L ? 0 : pw + 1;
+        prefetch(s + D, k);
+    };
+
+    const int total = KW + kWave - 1;
+    // rounds of U diagonals; while lanes are still starting (s < 64) the
+    // register state must not be overwritten by lanes with t < 0
+    const int ramp_end = REG ? min(total, (kWave + U - 1) / U * U) : 0;
+    int sb = 0;
+    for (; sb < ramp_end; sb += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) diagonal(sb + u, u, true);
+    }
+    for (; sb < total; sb += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) diagonal(sb + u, u, false);
+    }
+    if (lane == 0) {
+        if (spins) atomicAdd(&a.stats->stall_spins, (unsigned long long)spins);
+        atomicAdd(&a.stats->tile_steps, (unsigned long long)a.K);
+    }
+    if (__any(bad_range) && lane == 0) atomicAdd(&a.stats->ieee_diagonals, 1ull);
+}
+
+// {hx, src} per column, padded to ntj*W with the last column's values.
+__global__ void colc_kernel(Coeffs cf, d2 *colc, int ncols_pad)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncols_pad) return;
+    const int cc = min(c, cf.nx - 1);
+    const double ax = cf.alpha * cf.inv_dx[cc];
+    colc[c] = d2{0.5 * ax, cf.src[cc]};
+}
+
+__global__ void fill_sent_kernel(d2 *p, size_t n)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double s = __longlong_as_double((long long)kSentBits);
+    p[i] = d2{s, s};
+}
+
+// entry of state k (k >= 0) of local cell (lane, cl) of a tile
+__device__ __forceinline__ long long ring_entry(long long origin, long long L, int W, int k, int cl,
+                                                int lane)
+{
+    long long d = (long long)(k - 1) * W + cl + lane + origin;
+    d %= L;
+    return d < 0 ? d + L : d;
+}
+
+// C-order state w (u plane | v plane) -> ring entries of state 0.
+// Padding cells (rows >= ny, columns >= nx) get u = v = 1.
+__global__ void ring_load_kernel(StreamArgs a, int W, const double *w)
+{
+    const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t per_tile = (size_t)kWave * W;
+    if (i >= (size_t)a.ntiles * per_tile) return;
+    const int tile = (int)(i / per_tile);
+    const int rem = (int)(i - (size_t)tile * per_tile);
+    const int lane = rem % kWave, cl = rem / kWave;
+    const int ti = tile / a.ntj, tj = tile % a.ntj;
+    const int row = ti * kWave + lane, col = tj * W + cl;
+    const size_t n = (size_t)a.cf.nx * a.cf.ny;
+    d2 v{1.0, 1.0};
+    if (row < a.cf.ny && col < a.cf.nx) {
+        const size_t j = (size_t)row * a.cf.nx + col;
+        v = d2{w[j], w[n + j]};
+    }
+    a.ring[((size_t)tile * a.L + ring_entry(a.origin, a.L, W, 0, cl, lane)) * kWave + lane] = v;
+}
+
+// Snapshot extraction: out[e * ldo + j] = element e of state (k0 + j*kstep),
+// e over the 2*nx*ny C-order state (u plane | v plane), j < count.
+__global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int count,
+                                    double *out, int ldo)
+{
+    const size_t n = (size_t)a.cf.nx * a.cf.ny;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n * count) return;
+    const size_t cell = idx / count;
+    const int j = (int)(idx - cell * count);
+    const int row = (int)(cell / a.cf.nx), col = (int)(cell - (size_t)row * a.cf.nx);
+    const int ti = row / kWave, lane = row - ti * kWave;
+    const int tj = col / W, cl = col - tj * W;
+    const int tile = ti * a.ntj + tj;
+    const d2 v = a.ring[((size_t)tile * a.L +
+                         ring_entry(a.origin, a.L, W, k0 + j * kstep, cl, lane)) *
+                            kWave +
+                        lane];
+    out[cell * ldo + j] = v.x;
+    out[(n + cell) * ldo + j] = v.y;
+}
+
+template <int W, int D>
+int launch_w(const StreamArgs &a, int blocks, hipStream_t st)
+{
+    hipLaunchKernelGGL((stream_kernel<W, D>), dim3(blocks), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+StreamPlan plan_stream(int nx, int ny, int tiles_target, int w_force)
+{
+    StreamPlan p{};
+    p.nti = (ny + kWave - 1) / kWave;
+    int W = 8;
+    if (w_force > 0) {
+        W = w_force;
+    } else {
+        // smallest power-of-two width (>= 8) whose tile count fits the target
+        while (W < 4096 && (long long)p.nti * ((nx + W - 1) / W) > tiles_target) W *= 2;
+    }
+    p.W = W;
+    p.ntj = (nx + W - 1) / W;
+    p.ntiles = p.nti * p.ntj;
+    p.R = 4;
+    while (p.R < 64 / W + 4) p.R *= 2;
+    return p;
+}
+
+bool stream_width_supported(int W)
+{
+    return W == 8 || W == 16 || W == 32 || W == 64 || W == 128 || W == 256 || W == 512 ||
+           W == 1024 || W == 2048 || W == 4096;
+}
+
+int launch_stream(const StreamArgs &a, int W, hipStream_t st)
+{
+    const int blocks = (a.ntiles + 3) / 4;
+    switch (W) {
+    case 8: return launch_w<8, 4>(a, blocks, st);
+    case 16: return launch_w<16, 8>(a, blocks, st);
+    case 32: return launch_w<32, 8>(a, blocks, st);
+    case 64: return launch_w<64, 8>(a, blocks, st);
+    case 128: return launch_w<128, 8>(a, blocks, st);
+    case 256: return launch_w<256, 8>(a, blocks, st);
+    case 512: return launch_w<512, 8>(a, blocks, st);
+    case 1024: return launch_w<1024, 8>(a, blocks, st);
+    case 2048: return launch_w<2048, 8>(a, blocks, st);
+    case 4096: return launch_w<4096, 8>(a, blocks, st);
+    default: return -1;
+    }
+}
+
+int stream_max_resident_blocks(int W, int *per_cu, int *cus)
+{
+    int dev = 0, n = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -3;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return -3;
+    const void *fn = nullptr;
+    switch (W) {
+    case 8: fn = (const void *)stream_kernel<8, 4>; break;
+    case 16: fn = (const void *)stream_kernel<16, 8>; break;
+    case 32: fn = (const void *)stream_kernel<32, 8>; break;
+    case 64: fn = (const void *)stream_kernel<64, 8>; break;
+    case 128: fn = (const void *)stream_kernel<128, 8>; break;
+    case 256: fn = (const void *)stream_kernel<256, 8>; break;
+    case 512: fn = (const void *)stream_kernel<512, 8>; break;
+    case 1024: fn = (const void *)stream_kernel<1024, 8>; break;
+    case 2048: fn = (const void *)stream_kernel<2048, 8>; break;
+    case 4096: fn = (const void *)stream_kernel<4096, 8>; break;
+    default: return -1;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0) != hipSuccess) return -3;
+    // the API can over-report by one block per CU (MI355X_MICROARCH.md, residency)
+    n = n > 1 ? n - 1 : n;
+    if (per_cu) *per_cu = n;
+    if (cus) *cus = ncu;
+    return n * ncu;
+}
+
+int launch_colc(const Coeffs &cf, int ncols_pad, void *colc, hipStream_t st)
+{
+    hipLaunchKernelGGL(colc_kernel, dim3((ncols_pad + 255) / 256), dim3(256), 0, st, cf,
+                       (d2 *)colc, ncols_pad);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_fill_sentinel(void *p, size_t n16, hipStream_t st)
+{
+    if (n16 == 0) return 0;
+    hipLaunchKernelGGL(fill_sent_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, st,
+                       (d2 *)p, n16);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st)
+{
+    const size_t total = (size_t)a.ntiles * kWave * W;
+    hipLaunchKernelGGL(ring_load_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                       a, W, w);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
+                        int ldo, hipStream_t st)
+{
+    const size_t total = (size_t)a.cf.nx * a.cf.ny * count;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(ring_extract_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       st, a, W, k0, kstep, count, out, ldo);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+}  // namespace burg

@@ -65,14 +65,17 @@ def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
 
 
 def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
-                                snap_every=1, device=0, tile_w=64, tol=DEFAULT_TOL,
-                                par_passes=0, verbose=1, allow_nonsquare=False,
+                                snap_every=1, device=0, engine="stream", tile_w=64,
+                                tol=DEFAULT_TOL, par_passes=0, verbose=1, allow_nonsquare=False,
                                 newton_max_its=100, newton_rtol=1e-12, return_stats=False):
     """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM
     (C/hypernet2D.py:72-131) on an MI355X.
 
     solver="march" (default) solves each implicit step exactly with the
-    closed-form upwind march; solver="newton" runs the reference algorithm
+    closed-form upwind march, by default on the streaming engine (all steps
+    in one pipelined launch, bitwise the sequential march; engine="tiles"
+    selects the per-step block-Jacobi tile engine, tuned by tile_w / tol /
+    par_passes); solver="newton" runs the reference algorithm
     (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
     Both return the reference's snapshot matrix.  verbose=1 prints the
     reference's header line; verbose=2 also the per-step lines
@@ -81,7 +84,7 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     if verbose:
         print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mu, device, allow_nonsquare, tile_w=tile_w,
-                   par_passes=par_passes, tol=tol)
+                   par_passes=par_passes, tol=tol, engine=engine)
     snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
                                      solver, newton_max_its, newton_rtol, int(snap_every))
     if verbose >= 2:

@@ -20,7 +20,7 @@ class FOMContext:
     """A grid (nx x ny) resident on one GPU."""
 
     def __init__(self, nx, ny, device=0, tile_w=64, par_passes=0, tol=DEFAULT_TOL,
-                 profile=False):
+                 profile=False, engine="stream", stream_w=0, tiles_target=0):
         self._L = _lib.load()
         self.nx, self.ny, self.device = int(nx), int(ny), int(device)
         h = ctypes.c_void_p()
@@ -28,6 +28,7 @@ class FOMContext:
         self._h = h
         self._problem = None
         self.set_options(tile_w, par_passes, tol, profile)
+        self.set_engine(engine, stream_w, tiles_target)
 
     @property
     def m(self):
@@ -48,6 +49,14 @@ class FOMContext:
         _lib.check(self._L.burg_set_options(self._h, int(tile_w), int(par_passes), float(tol),
                                             1 if profile else 0))
         self.options = dict(tile_w=tile_w, par_passes=par_passes, tol=tol, profile=profile)
+
+    def set_engine(self, engine="stream", stream_w=0, tiles_target=0):
+        """March engine: "stream" (exact pipelined march, one launch per run
+        chunk; the default) or "tiles" (block-Jacobi tile passes per step,
+        tuned by set_options)."""
+        _lib.check(self._L.burg_set_engine(self._h, _lib.ENGINES[engine], int(stream_w),
+                                           int(tiles_target)))
+        self.engine = dict(engine=engine, stream_w=stream_w, tiles_target=tiles_target)
 
     def set_problem(self, grid_x, grid_y, dt, mu, allow_nonsquare=False):
         key = (np.asarray(grid_x).tobytes(), np.asarray(grid_y).tobytes(), float(dt),
@@ -134,11 +143,17 @@ def get_context(nx, ny, device=0, **opts):
     if d is None:
         d = _cache.ctxs = {}
     key = (int(device), int(nx), int(ny))
+    eopts = {k: opts.pop(k) for k in ("engine", "stream_w", "tiles_target") if k in opts}
     ctx = d.get(key)
     if ctx is None:
-        ctx = d[key] = FOMContext(nx, ny, device, **opts)
-    elif opts and any(ctx.options.get(k) != v for k, v in opts.items()):
+        ctx = d[key] = FOMContext(nx, ny, device, **opts, **eopts)
+        return ctx
+    if opts and any(ctx.options.get(k) != v for k, v in opts.items()):
         merged = dict(ctx.options)
         merged.update(opts)
         ctx.set_options(**merged)
+    if eopts and any(ctx.engine.get(k) != v for k, v in eopts.items()):
+        merged = dict(ctx.engine)
+        merged.update(eopts)
+        ctx.set_engine(**merged)
     return ctx

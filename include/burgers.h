@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 1
+#define BURG_ABI_VERSION 2
 
 enum burg_status {
     BURG_OK = 0,
@@ -73,7 +73,18 @@ typedef struct burg_stats {
     int64_t march_launches;     /* profiling mode: march kernel launches timed */
     double last_rel;            /* newton solver: last step's final ||R||/||R0|| */
     int64_t tail_passes;        /* passes finished by the final kernel's last workgroup */
+    int32_t engine;             /* march engine used: BURG_ENGINE_* */
+    int32_t stream_w;           /* streaming engine: tile width (columns) */
+    int64_t stream_tiles;       /* streaming engine: tiles (= wavefronts) per launch */
+    int64_t stall_spins;        /* streaming engine: polls of not-yet-ready edge data */
+    int64_t slow_diagonals;     /* streaming engine: diagonals that took the slow path */
+    int64_t stream_launches;    /* streaming engine: launches (one per run chunk) */
 } burg_stats;
+
+enum burg_engine {
+    BURG_ENGINE_STREAM = 0,  /* one launch for many steps: exact pipelined march (default) */
+    BURG_ENGINE_TILES = 1    /* one step at a time: block-Jacobi tile passes (burg_set_options) */
+};
 
 int burg_abi_version(void);
 const char *burg_last_error(void);
@@ -108,6 +119,13 @@ int burg_set_problem(burg_ctx *ctx, const double *inv_dx, const double *inv_dy,
  * re-marched (0 = bitwise fixed point = the sequential march).
  * profile: 1 = time every march launch with HIP events (burg_stats). */
 int burg_set_options(burg_ctx *ctx, int tile_w, int par_passes, double tol, int profile);
+
+/* March engine selection.  engine: BURG_ENGINE_*.  stream_w: streaming tile
+ * width, a power of two in [8, 4096] (0: automatic, the narrowest width whose
+ * tile count fits tiles_target).  tiles_target: wavefronts to aim for
+ * (0: 1024 = one per SIMD of the MI355X).  The tile count is always capped by
+ * what the device keeps resident at once (the engine needs every tile live). */
+int burg_set_engine(burg_ctx *ctx, int engine, int stream_w, int tiles_target);
 
 /* Parity hooks (whole-grid host arrays; single-GPU contexts only). */
 int burg_residual(burg_ctx *ctx, const double *w, const double *wp, double *r,

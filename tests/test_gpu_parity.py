@@ -85,7 +85,7 @@ def test_march_step_bitwise_sequential(gpu, orc, N, tw, par):
     ~#tile rows passes in y-uniform regions: exercises the tail path)."""
     P = orc.Problem(N)
     wp = state_after(orc, P, 7)
-    ctx = make_ctx(N, tile_w=tw, tol=0.0, par_passes=par)
+    ctx = make_ctx(N, tile_w=tw, tol=0.0, par_passes=par, engine="tiles")
     snaps, st, its, _ = ctx.run(wp, 1)
     assert st["unconverged_steps"] == 0
     assert np.array_equal(snaps[:, 1], P.march_step(wp))
@@ -99,12 +99,75 @@ def test_march_step_bitwise_tiled_schedule(gpu, orc, N, tw, par):
     to the final kernel's last workgroup (the tail path)."""
     P = orc.Problem(N)
     wp = state_after(orc, P, 20)
-    ctx = make_ctx(N, tile_w=tw, tol=TOL4ULP, par_passes=par)
+    ctx = make_ctx(N, tile_w=tw, tol=TOL4ULP, par_passes=par, engine="tiles")
     snaps, st, its, _ = ctx.run(wp, 1)
     ws, k, _ = P.march_tiled(wp, tw=tw, tol=TOL4ULP)
     assert np.array_equal(snaps[:, 1], ws)
     assert its[0] == k
     assert rel(ws, P.march_step(wp)) <= 1e-14
+
+
+# ------------------------------------------------------ streaming engine --
+@pytest.mark.parametrize("N,ny,W,tiles,T", [
+    (13, 13, 8, 0, 5), (64, 64, 16, 0, 4), (100, 100, 0, 0, 6), (250, 250, 0, 0, 5),
+    (250, 250, 64, 0, 3), (333, 333, 32, 0, 3), (130, 70, 8, 0, 4), (96, 200, 16, 0, 4),
+    (512, 512, 0, 4096, 2), (300, 300, 256, 0, 3), (200, 129, 0, 64, 7)])
+def test_stream_bitwise_sequential_march(gpu, orc, N, ny, W, tiles, T):
+    """The streaming engine IS the sequential march: every snapshot bit-equal
+    to the oracle's orc_march_step trajectory, for any tiling (partial tiles,
+    partial strips, non-square grids, one tile column, many tiles)."""
+    P = orc.Problem(N, ny, Ly=100.0 * ny / N, allow_nonsquare=(N != ny))
+    w0 = state_after(orc, P, 3)
+    ctx = FOMContext_for(N, ny, engine="stream", stream_w=W, tiles_target=tiles)
+    ctx.set_problem(P.grid_x, P.grid_y, P.dt, P.mu, allow_nonsquare=(N != ny))
+    snaps, st, its, _ = ctx.run(w0, T)
+    ref, _, _ = P.fom(w0, T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+    assert st["engine"] == 0 and st["steps"] == T and st["stream_launches"] == 1
+    assert st["tile_marches"] == T * st["stream_tiles"]
+    assert np.all(its == 1)
+
+
+def FOMContext_for(nx, ny, **opts):
+    from finitedifference_amd.solver import FOMContext
+    return FOMContext(nx, ny, **opts)
+
+
+@pytest.mark.parametrize("chunk", [1, 3, 7])
+def test_stream_chunked_run_and_snap_every(gpu, orc, monkeypatch, chunk):
+    """Runs longer than the ring (forced small chunks) and snap_every > 1 give
+    the same columns as one long launch."""
+    N, T = 96, 12
+    P = orc.Problem(N)
+    w0 = np.ones(P.m)
+    ref, _, _ = P.fom(w0, T)
+    monkeypatch.setenv("BURG_STREAM_CHUNK", str(chunk))
+    ctx = make_ctx(N, engine="stream", stream_w=16)
+    snaps, st, _, _ = ctx.run(w0, T)
+    assert st["stream_launches"] == -(-T // chunk)
+    assert all(np.array_equal(snaps[:, j], ref[j]) for j in range(T + 1))
+    sub, _, _, _ = ctx.run(w0, T, snap_every=5)
+    assert sub.shape == (P.m, T // 5 + 1)
+    assert all(np.array_equal(sub[:, j], ref[5 * j]) for j in range(T // 5 + 1))
+
+
+def test_stream_advance_matches_run(gpu, orc):
+    N = 200
+    P = orc.Problem(N)
+    ref, _, _ = P.fom(np.ones(P.m), 9)
+    ctx = make_ctx(N, engine="stream")
+    ctx.upload(np.ones(P.m))
+    for k in (2, 3, 4):  # several launches continue the same trajectory
+        ctx.advance(k)
+    assert np.array_equal(ctx.download(), ref[9])
+
+
+def test_stream_and_tiles_engines_agree_at_tol0(gpu):
+    N, T = 160, 5
+    a = make_ctx(N, engine="stream").run(np.ones(2 * N * N), T)[0]
+    b = make_ctx(N, engine="tiles", tol=0.0).run(np.ones(2 * N * N), T)[0]
+    assert np.array_equal(a, b)
 
 
 def test_march_solves_the_reference_residual(gpu):
@@ -163,7 +226,9 @@ def test_coarse250_full_run_vs_reference(gpu, orc):
     steps = g["slice_steps"]
     assert rel(U[N // 2, :, steps].T, g["u_row"].T) <= REF_TOL
     ws = orc.Problem(N).fom(np.ones(2 * n), T)[0]
-    assert max(rel(snaps[:, j], ws[j]) for j in range(1, T + 1, 7)) <= 1e-13
+    # streaming engine = the sequential march, bit for bit, over all 500 steps
+    assert all(np.array_equal(snaps[:, j], ws[j]) for j in range(0, T + 1, 7))
+    assert np.array_equal(snaps[:, T], ws[T])
 
 
 def test_fine750_vs_author_pickle(gpu):
@@ -188,9 +253,10 @@ def test_snap_every_layout(gpu):
     assert np.array_equal(sub, full[:, ::4])
 
 
-def test_device_resident_advance_matches_run(gpu):
+@pytest.mark.parametrize("engine", ["stream", "tiles"])
+def test_device_resident_advance_matches_run(gpu, engine):
     N, T = 128, 9
-    ctx = make_ctx(N)
+    ctx = make_ctx(N, engine=engine)
     full, _, _, _ = ctx.run(np.ones(2 * N * N), T)
     ctx.upload(np.ones(2 * N * N))
     st = ctx.advance(T)
