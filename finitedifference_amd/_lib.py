@@ -52,6 +52,7 @@ class BurgStats(ctypes.Structure):
         ("stall_spins", ctypes.c_int64),
         ("slow_diagonals", ctypes.c_int64),
         ("stream_launches", ctypes.c_int64),
+        ("slow_ticks", ctypes.c_int64),
     ]
 
     def as_dict(self):

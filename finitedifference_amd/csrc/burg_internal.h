@@ -66,11 +66,20 @@ struct d2 {
 struct StreamStats {
     unsigned long long tile_steps;      // tile x step units marched
     unsigned long long stall_spins;     // slow-path polls of not-yet-ready mailboxes
-    unsigned long long ieee_diagonals;  // diagonals re-run with IEEE sqrt/div (range)
+    unsigned long long ieee_diagonals;  // waves that took the slow path at least once
+    unsigned long long slow_diagonals;  // diagonals that took the slow path (all waves)
+    unsigned long long slow_ticks;      // s_memtime ticks spent in the slow path
+    unsigned long long why[6];          // slow-path causes: 0 east slot busy, 1 north slot
+                                        // busy, 2 west not written, 3 south not written,
+                                        // 4 range (IEEE redo), 5 entries that needed a re-poll
 };
 
 // Tiling of a slab for the streaming engine: nti strips of 64 rows, ntj tiles
 // of W columns; R mailbox slots (steps) per edge.
+// Bytes per edge granule slot: one 128-B L2 line each, so that reading one
+// granule never caches a neighbour granule before its producer wrote it.
+constexpr int kGranuleStride = 128;
+
 struct StreamPlan {
     int W, nti, ntj, ntiles, R;
 };

@@ -314,7 +314,10 @@ int stream_setup(burg_ctx *c)
             p = plan_stream(c->nx, c->nrows, 0, p.W * 2);
         }
         c->sp = p;
-        c->box16 = (size_t)p.ntiles * p.R * (kWave + p.W);
+        c->box16 = (size_t)p.ntiles * p.R * (kWave + p.W) * (kGranuleStride / sizeof(d2));
+        if (c->box16 * sizeof(d2) >= (1ull << 31))
+            return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB (%d tiles of width %d)",
+                        p.ntiles, p.W);
         if (int e = dalloc(&c->d_boxes, c->box16)) return e;
         if (int e = dalloc(&c->d_colc, (size_t)p.ntj * p.W)) return e;
         if (int e = dalloc(&c->d_err, 4)) return e;
@@ -349,9 +352,9 @@ StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
     a.colc = c->d_colc;
     a.ring = c->d_ring;
     a.wbox = c->d_boxes;
-    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * c->sp.R * kWave;
-    a.wbox_bytes = (size_t)c->sp.ntiles * c->sp.R * kWave * sizeof(d2);
-    a.sbox_bytes = (size_t)c->sp.ntiles * c->sp.R * c->sp.W * sizeof(d2);
+    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * c->sp.R * kWave * (kGranuleStride / sizeof(d2));
+    a.wbox_bytes = (size_t)c->sp.ntiles * c->sp.R * kWave * kGranuleStride;
+    a.sbox_bytes = (size_t)c->sp.ntiles * c->sp.R * c->sp.W * kGranuleStride;
     a.origin = origin;
     a.L = L;
     a.K = K;
@@ -413,7 +416,14 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->stream_w = c->sp.W;
         st->stream_tiles = c->sp.ntiles;
         st->stall_spins = (int64_t)ss.stall_spins;
-        st->slow_diagonals = (int64_t)ss.ieee_diagonals;
+        st->slow_diagonals = (int64_t)ss.slow_diagonals;
+        if (const char *e = std::getenv("BURG_STREAM_DEBUG"))  // diagnostics
+            if (std::atoi(e) & 8)
+                std::fprintf(stderr,
+                             "[stream] slow-path causes: east-busy %llu north-busy %llu "
+                             "west-unwritten %llu south-unwritten %llu range %llu repoll %llu\n",
+                             ss.why[0], ss.why[1], ss.why[2], ss.why[3], ss.why[4], ss.why[5]);
+        st->slow_ticks = (int64_t)ss.slow_ticks;
         st->stream_launches = launches;
     }
     return 0;

@@ -31,6 +31,8 @@
 // sentinel before reusing it R steps later.  No fences, no counters
 // (MI355X_MICROARCH.md, hand-off forms R2).  Every wait is bounded: a wave that
 // gives up sets the error word and the launch still drains.
+#include <cstdlib>
+
 #include "burg_internal.h"
 #include "cell_math.h"
 
@@ -85,22 +87,42 @@ __device__ __forceinline__ v4u ld_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off)
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
 }
 
+__device__ __forceinline__ v4u ld_plain(__amdgpu_buffer_rsrc_t rs, unsigned off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+}
+
 __device__ __forceinline__ void st_sc1(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 16);
+}
+
+__device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
 }
 
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
 
 // One wavefront per tile; 4 tiles per workgroup (one per SIMD).
-template <int W, int D>
+template <int W, int D, int DM>
 __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
 {
     static_assert((W & (W - 1)) == 0 && W > D, "W: power of two > D");
+    static_assert(D % DM == 0, "mailbox slots must tile the unroll");
     constexpr int LW = ilog2<W>();
+    // Narrow tiles (W <= 32) keep each lane's last W states in LDS: the
+    // previous step of the cell of diagonal s is the lane's own output of
+    // diagonal s - W, i.e. LDS slot s mod W.  Wider tiles read it back from
+    // the tile's ring in HBM (ring entry s - W, prefetched D diagonals ahead).
+    constexpr bool LDSST = W <= 32;
+    constexpr bool LDSCC = W <= 1024;  // column table in LDS (else prefetched from HBM)
+    __shared__ v4u lds_st[LDSST ? 4 * W * kWave : 1];  // [wave][s mod W][lane]
+    __shared__ v4u lds_cc[LDSCC ? 4 * W : 1];          // [wave][column] {hx, src}
+    const int wave = threadIdx.x >> 6;
     const int lane = threadIdx.x & (kWave - 1);
-    const int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int tile = __builtin_amdgcn_readfirstlane(blockIdx.x * 4 + wave);
     if (tile >= a.ntiles) return;
     const int ti = tile / a.ntj, tj = tile - ti * a.ntj;
     const int ny = a.cf.ny;
@@ -120,47 +142,63 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
     const double lb = a.cf.lbc[r];
     const bool col0_tile = tj == 0;
 
-    const d2 *__restrict__ colc = a.colc + (size_t)tj * W;
-    const d2 *ringt = a.ring + (size_t)tile * a.L * kWave;
-    d2 *ringw = a.ring + (size_t)tile * a.L * kWave;
+    // the tile's ring (L entries of 64 x 16 B) in HBM
+    const __amdgpu_buffer_rsrc_t ring = __builtin_amdgcn_make_buffer_rsrc(
+        a.ring + (size_t)tile * a.L * kWave, 0, (int)(a.L * kWave * 16), 0x00020000);
+    const unsigned lane16 = lane * 16u;
     const __amdgpu_buffer_rsrc_t wbox =
         __builtin_amdgcn_make_buffer_rsrc(a.wbox, 0, (int)a.wbox_bytes, 0x00020000);
     const __amdgpu_buffer_rsrc_t sbox =
         __builtin_amdgcn_make_buffer_rsrc(a.sbox, 0, (int)a.sbox_bytes, 0x00020000);
-    // mailbox byte offsets: west box of tile t, slot q, row l: ((t*R + q)*64 + l)*16;
-    // south box of tile t, slot q, column c: ((t*R + q)*W + c)*16
-    const unsigned wb_mine = (unsigned)tile * a.R * kWave * 16u + lane * 16u;
-    const unsigned wb_step = (unsigned)a.R * kWave * 16u;  // -> the east tile's box
-    const unsigned sb_mine = (unsigned)tile * a.R * W * 16u;
-    const unsigned sb_step = (unsigned)a.ntj * a.R * W * 16u;  // -> the north tile's box
+    // mailbox byte offsets (G = kGranuleStride): west box of tile t, slot q,
+    // row l: ((t*R + q)*64 + l)*G; south box of tile t, slot q, column c:
+    // ((t*R + q)*W + c)*G
+    constexpr unsigned G = kGranuleStride;
+    const unsigned wb_mine = (unsigned)tile * a.R * kWave * G + lane * G;
+    const unsigned wb_step = (unsigned)a.R * kWave * G;  // -> the east tile's box
+    const unsigned sb_mine = (unsigned)tile * a.R * W * G;
+    const unsigned sb_step = (unsigned)a.ntj * a.R * W * G;  // -> the north tile's box
     const v4u sent = as_v4u(__longlong_as_double((long long)kSentBits),
                             __longlong_as_double((long long)kSentBits));
-
-    // ring positions (diagonal -> entry), wave-uniform
     const long long L = a.L;
-    long long pw = a.origin;                         // entry of diagonal s
-    long long pr = ((a.origin - W) % L + L) % L;    // entry read by the next prefetch
-                                                     // (diagonal sp - W for sp = 0, 1, ...)
 
-    // Per slot i (diagonal s = i mod D), prefetched D diagonals ahead:
+    // column table and (LDSST) state 0 into LDS: state 0 of the lane's column
+    // c sits at diagonal c + lane - W, i.e. LDS slot (c + lane) mod W
+    v4u *my_st = lds_st + (LDSST ? wave * W * kWave : 0);
+    v4u *my_cc = lds_cc + (LDSCC ? wave * W : 0);
+    const __amdgpu_buffer_rsrc_t colc = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(a.colc + (size_t)tj * W), 0, W * 16, 0x00020000);
+    if constexpr (LDSCC) {
+        for (int c = lane; c < W; c += kWave) {
+            const d2 v = a.colc[(size_t)tj * W + c];
+            my_cc[c] = as_v4u(v.x, v.y);
+        }
+    }
+    if constexpr (LDSST) {
+        for (int c = 0; c < W; ++c) {
+            long long e = (a.origin + c + lane - W) % L;
+            e = e < 0 ? e + L : e;
+            my_st[((c + lane) & (W - 1)) * kWave + lane] = ld_plain(ring, (unsigned)e * 1024u + lane16);
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_s_waitcnt(0);
+
+    // Prefetch rings.  Edge granules, DM diagonals ahead (slot j = s mod DM):
     //   gw: the lane's west/east granule -- at column 0 the west inflow of this
     //       step (consume), at column W-1 the east tile's slot (must be empty)
     //   gs: lane 0: the south inflow granule; lane `top`: the north tile's slot
     //   ow, os: the byte offsets of gw, gs (kOOB where the lane has no access:
     //       buffer loads there return 0 and stores are dropped)
-    // and, for wide tiles (!REG), pf: the lane's state of the previous step
-    // (ring entry s - W) and cc: {hx, src} of the lane's column.
-    // Narrow tiles (REG, W <= 16) keep both in registers instead: the lane's
-    // previous-step state of diagonal s is its own output of diagonal s - W,
-    // i.e. the same unrolled slot one round earlier, and its column at slot i
-    // is (i - lane) mod W every round.
-    constexpr bool REG = W <= 16;
-    constexpr int U = REG ? W : D;  // unroll (diagonals per round)
-    static_assert(U % D == 0, "prefetch slots must tile the unroll");
-    v4u gw[D], gs[D];
-    unsigned ow[D], os[D];
-    d2 pf[REG ? 1 : D], cc[REG ? 1 : D];
-    d2 st[REG ? W : 1], ccr[REG ? W : 1];
+    // DM is short on purpose: a pipelined consumer runs just behind its
+    // producer, and a granule fetched too early is still the sentinel.
+    // State and columns of wide tiles, D diagonals ahead (slot i = s mod D):
+    //   pf (!LDSST): the lane's previous-step state (ring entry s - W)
+    //   cc (!LDSCC): {hx, src} of the lane's column
+    v4u gw[DM], gs[DM], pf[LDSST ? 1 : D], cc[LDSCC ? 1 : D];
+    unsigned ow[DM], os[DM];
+    long long pw = a.origin;                       // ring entry of diagonal s
+    long long pr = ((a.origin - W) % L + L) % L;  // ring entry of the next prefetch's s - W
     const int lane_j = lane;  // keep lane in a VGPR
     // bases with the tile's neighbourhood folded in (kOOB: no such neighbour).
     // Padding lanes (rows past the grid in a partial strip) stay out of the
@@ -171,52 +209,51 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
     // lane 0 consumes the south edge, lane `top` produces the north edge
     const unsigned slb = lane == 0 ? (has_south ? sb_mine : kOOB)
                                    : (lane == top && has_north ? sb_mine + sb_step : kOOB);
-    auto prefetch = [&](int sp, int i) {
+    auto prefetch_ring = [&](int sp, int i) {
+        const int cp = (sp - lane_j) & (W - 1);
+        if constexpr (!LDSST) {
+            pf[i % (LDSST ? 1 : D)] = ld_plain(ring, (unsigned)pr * 1024u + lane16);
+            pr = pr + 1 == L ? 0 : pr + 1;
+        }
+        if constexpr (!LDSCC) cc[i % (LDSCC ? 1 : D)] = ld_plain(colc, (unsigned)cp * 16u);
+    };
+    auto prefetch_mail = [&](int sp, int j) {
         const int tp = sp - lane_j;
         const int cp = tp & (W - 1);
         const unsigned qp = (unsigned)(tp >> LW) & (unsigned)Rm;
         const bool vp = (unsigned)tp < (unsigned)KW;
-        if constexpr (!REG) {
-            pf[i] = ringt[(size_t)pr * kWave + lane];
-            cc[i] = colc[cp];
-            pr = pr + 1 == L ? 0 : pr + 1;
-        }
         const unsigned o = cp == 0 ? wcb : (cp == W - 1 ? wpb : kOOB);
-        ow[i] = vp ? o + (qp << 10) : kOOB;
-        gw[i] = ld_sc1(wbox, ow[i]);
-        os[i] = vp ? slb + ((qp << LW) | (unsigned)cp) * 16u : kOOB;
-        gs[i] = ld_sc1(sbox, os[i]);
+        ow[j] = vp ? o + qp * (kWave * G) : kOOB;
+        gw[j] = ld_sc1(wbox, ow[j]);
+        os[j] = vp ? slb + ((qp << LW) | (unsigned)cp) * G : kOOB;
+        gs[j] = ld_sc1(sbox, os[j]);
     };
-
-    if constexpr (REG) {
-        // state 0 of column (i - lane) mod W sits at diagonal c + lane - W
 #pragma unroll
-        for (int i = 0; i < W; ++i) {
-            const int c = (i - lane_j) & (W - 1);
-            long long e = (a.origin + c + lane_j - W) % L;
-            e = e < 0 ? e + L : e;
-            st[i] = ringt[(size_t)e * kWave + lane];
-            ccr[i] = colc[c];
-        }
-    }
+    for (int i = 0; i < D; ++i) prefetch_ring(i, i);
 #pragma unroll
-    for (int i = 0; i < D; ++i) prefetch(i, i);
+    for (int j = 0; j < DM; ++j) prefetch_mail(j, j);
+    // Land the first slots here: otherwise the compiler's wait counts at the
+    // loop head are those of this short prologue path (few operations after
+    // each load) and every round would wait on its newest write-through stores.
+    __builtin_amdgcn_s_waitcnt(0);
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
-    unsigned spins = 0;
+    unsigned spins = 0, slow_n = 0, why_n[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long slow_t = 0;
     bool bad_range = false;
 
-    // one diagonal: slot k of the prefetch ring, u of the unroll
-    auto diagonal = [&](const int s, const int u, const bool ramp) {
-        const int k = u % D;
+    // one diagonal s, prefetch slots k = s mod D, m = s mod DM
+    auto diagonal = [&](const int s, const int k) {
+        const int m = k % DM;
         const int t = s - lane_j;
         const int c = t & (W - 1);
         const bool valid = (unsigned)t < (unsigned)KW;
         const bool at0 = c == 0, atE = c == W - 1;
         const bool s_in = lane == 0, n_out = lane == top && lane != 0;
+        v4u *st_slot = my_st + (LDSST ? (s & (W - 1)) * kWave + lane : 0);
         // ---- the cell (MarchCell::pre + chain, same op order)
-        const d2 x = REG ? st[u % (REG ? W : 1)] : pf[k % (REG ? 1 : D)];
-        const d2 co = REG ? ccr[u % (REG ? W : 1)] : cc[k % (REG ? 1 : D)];
+        const d2 x = as_d2(LDSST ? *st_slot : pf[k % (LDSST ? 1 : D)]);
+        const d2 co = as_d2(LDSCC ? my_cc[c] : cc[k % (LDSCC ? 1 : D)]);
         const double pu = x.x, pv = x.y;
         const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
         const double sl = (col0_tile && at0) ? co.y + lb : co.y;
@@ -232,41 +269,52 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
         const MarchCell::Row rw{ay, hy, lb};
         // producers: the east / north slot must be empty (sentinel in both halves)
         bool pbad = false;
-        if (has_east) pbad |= valid && rowok && atE && !all_sent(gw[k]);
-        if (has_north) pbad |= valid && n_out && !all_sent(gs[k]);
+        if (has_east) pbad |= valid && rowok && atE && !all_sent(gw[m]);
+        if (has_north) pbad |= valid && n_out && !all_sent(gs[m]);
         // west inflow at column 0: the granule, or +0.0 at the domain
         // boundary (the load was out of range); south inflow of lane 0 likewise.
         // A granule not yet written holds the sentinel NaN, which fails the
         // chain's range check: the slow path below then waits for it.
         if (at0) {
-            const d2 g = as_d2(gw[k]);
+            const d2 g = as_d2(gw[m]);
             e0 = g.x;
             e1 = g.y;
         }
-        double n0 = shr1_or(as_d2(gs[k]).x, no0);
-        double n1 = shr1_or(as_d2(gs[k]).y, no1);
+        double n0 = shr1_or(as_d2(gs[m]).x, no0);
+        double n1 = shr1_or(as_d2(gs[m]).y, no1);
         double oe0, oe1, on0, on1, o0, o1;
         bool ok;
         MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
         if (__builtin_expect(__any((!ok && valid && rowok) || pbad), 0)) {
             // slow path: poll the granules until inputs are written and
             // output slots are free, then redo the cell with IEEE sqrt/div
+            const unsigned long long t_in = __builtin_amdgcn_s_memtime();
+            if (has_east && __any(valid && rowok && atE && !all_sent(gw[m]))) ++why_n[0];
+            if (has_north && __any(valid && n_out && !all_sent(gs[m]))) ++why_n[1];
+            if (has_west && __any(valid && rowok && at0 && has_sent(gw[m]))) ++why_n[2];
+            if (has_south && __any(valid && s_in && has_sent(gs[m]))) ++why_n[3];
+            if (__any(!ok && valid && rowok && !(at0 && has_sent(gw[m])) &&
+                      !(s_in && has_sent(gs[m]))))
+                ++why_n[4];
+            bool first = true;
             for (;;) {
-                gw[k] = ld_sc1(wbox, ow[k]);
-                gs[k] = ld_sc1(sbox, os[k]);
+                gw[m] = ld_sc1(wbox, ow[m]);
+                gs[m] = ld_sc1(sbox, os[m]);
                 bool b = false;
-                if (has_west) b |= valid && rowok && at0 && has_sent(gw[k]);
-                if (has_south) b |= valid && s_in && has_sent(gs[k]);
-                if (has_east) b |= valid && rowok && atE && !all_sent(gw[k]);
-                if (has_north) b |= valid && n_out && !all_sent(gs[k]);
+                if (has_west) b |= valid && rowok && at0 && has_sent(gw[m]);
+                if (has_south) b |= valid && s_in && has_sent(gs[m]);
+                if (has_east) b |= valid && rowok && atE && !all_sent(gw[m]);
+                if (has_north) b |= valid && n_out && !all_sent(gs[m]);
                 if (!__any(b)) break;
+                if (first) ++why_n[5];
+                first = false;
                 if (++spins >= kSpinLimit) {
                     // report which wait gave up: tile, diagonal, and which edge
                     unsigned why = 0;
-                    if (has_west && __any(valid && rowok && at0 && has_sent(gw[k]))) why |= 1;
-                    if (has_south && __any(valid && s_in && has_sent(gs[k]))) why |= 2;
-                    if (has_east && __any(valid && rowok && atE && !all_sent(gw[k]))) why |= 4;
-                    if (has_north && __any(valid && n_out && !all_sent(gs[k]))) why |= 8;
+                    if (has_west && __any(valid && rowok && at0 && has_sent(gw[m]))) why |= 1;
+                    if (has_south && __any(valid && s_in && has_sent(gs[m]))) why |= 2;
+                    if (has_east && __any(valid && rowok && atE && !all_sent(gw[m]))) why |= 4;
+                    if (has_north && __any(valid && n_out && !all_sent(gs[m]))) why |= 8;
                     if (lane == 0 && atomicOr(a.err, 1u) == 0) {
                         a.err[1] = tile;
                         a.err[2] = s;
@@ -276,53 +324,54 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
                 }
                 __builtin_amdgcn_s_sleep(4);
             }
+            // back off once more: a consumer that keeps running exactly
+            // behind its producer finds every prefetched granule stale; a
+            // little extra lag lets the prefetches land after the writes
+            for (int q = (a.flags >> 8) & 0xff; q > 0; q -= 8) __builtin_amdgcn_s_sleep(8);
             if (at0) {
-                const d2 g = as_d2(gw[k]);
+                const d2 g = as_d2(gw[m]);
                 e0 = g.x;
                 e1 = g.y;
             }
-            n0 = shr1_or(as_d2(gs[k]).x, no0);
-            n1 = shr1_or(as_d2(gs[k]).y, no1);
+            n0 = shr1_or(as_d2(gs[m]).x, no0);
+            n1 = shr1_or(as_d2(gs[m]).y, no1);
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             bad_range = true;
+            ++slow_n;
+            slow_t += __builtin_amdgcn_s_memtime() - t_in;
         }
         e0 = oe0;
         e1 = oe1;
         no0 = on0;
         no1 = on1;
-        // ---- outputs
-        if constexpr (REG) {
-            // lanes that have not started keep their step-0 state
-            if (ramp) {
-                if (t >= 0) st[u % (REG ? W : 1)] = d2{o0, o1};
-            } else {
-                st[u % (REG ? W : 1)] = d2{o0, o1};
-            }
+        // ---- outputs (lanes that have not started keep their step-0 state)
+        const v4u out = as_v4u(o0, o1);
+        if constexpr (LDSST) {
+            if (t >= 0) *st_slot = out;
         }
-        if (valid) ringw[(size_t)pw * kWave + lane] = d2{o0, o1};
-        st_sc1(wbox, at0 ? ow[k] : kOOB, sent);                  // consumed: empty it
-        st_sc1(wbox, atE ? ow[k] : kOOB, as_v4u(oe0, oe1));      // east outflow
-        st_sc1(sbox, s_in ? os[k] : kOOB, sent);
-        st_sc1(sbox, s_in ? kOOB : os[k], as_v4u(on0, on1));     // north outflow
+        st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
+        st_sc1(wbox, at0 ? ow[m] : kOOB, sent);               // consumed: empty it
+        st_sc1(wbox, atE ? ow[m] : kOOB, as_v4u(oe0, oe1));   // east outflow
+        st_sc1(sbox, s_in ? os[m] : kOOB, sent);
+        st_sc1(sbox, s_in ? kOOB : os[m], as_v4u(on0, on1));  // north outflow
         pw = pw + 1 == L ? 0 : pw + 1;
-        prefetch(s + D, k);
+        prefetch_ring(s + D, k);
+        prefetch_mail(s + DM, m);
     };
 
     const int total = KW + kWave - 1;
-    // rounds of U diagonals; while lanes are still starting (s < 64) the
-    // register state must not be overwritten by lanes with t < 0
-    const int ramp_end = REG ? min(total, (kWave + U - 1) / U * U) : 0;
-    int sb = 0;
-    for (; sb < ramp_end; sb += U) {
+    for (int sb = 0; sb < total; sb += D) {
 #pragma unroll
-        for (int u = 0; u < U; ++u) diagonal(sb + u, u, true);
-    }
-    for (; sb < total; sb += U) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) diagonal(sb + u, u, false);
+        for (int k = 0; k < D; ++k) diagonal(sb + k, k);
     }
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, (unsigned long long)spins);
+        if (slow_n) {
+            atomicAdd(&a.stats->slow_diagonals, (unsigned long long)slow_n);
+            atomicAdd(&a.stats->slow_ticks, slow_t);
+            for (int q = 0; q < 6; ++q)
+                if (why_n[q]) atomicAdd(&a.stats->why[q], (unsigned long long)why_n[q]);
+        }
         atomicAdd(&a.stats->tile_steps, (unsigned long long)a.K);
     }
     if (__any(bad_range) && lane == 0) atomicAdd(&a.stats->ieee_diagonals, 1ull);
@@ -398,10 +447,10 @@ __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int 
     out[(n + cell) * ldo + j] = v.y;
 }
 
-template <int W, int D>
+template <int W, int D, int DM = 4>
 int launch_w(const StreamArgs &a, int blocks, hipStream_t st)
 {
-    hipLaunchKernelGGL((stream_kernel<W, D>), dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((stream_kernel<W, D, DM>), dim3(blocks), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -424,6 +473,10 @@ StreamPlan plan_stream(int nx, int ny, int tiles_target, int w_force)
     p.ntiles = p.nti * p.ntj;
     p.R = 4;
     while (p.R < 64 / W + 4) p.R *= 2;
+    if (const char *e = std::getenv("BURG_STREAM_R")) {  // diagnostics
+        const int v = std::atoi(e);
+        if (v >= 4 && (v & (v - 1)) == 0) p.R = v;
+    }
     return p;
 }
 
@@ -438,7 +491,8 @@ int launch_stream(const StreamArgs &a, int W, hipStream_t st)
     const int blocks = (a.ntiles + 3) / 4;
     switch (W) {
     case 8: return launch_w<8, 4>(a, blocks, st);
-    case 16: return launch_w<16, 8>(a, blocks, st);
+    case 16: return (a.flags & 2) ? launch_w<16, 8, 2>(a, blocks, st)
+                                  : launch_w<16, 8, 4>(a, blocks, st);
     case 32: return launch_w<32, 8>(a, blocks, st);
     case 64: return launch_w<64, 8>(a, blocks, st);
     case 128: return launch_w<128, 8>(a, blocks, st);
@@ -459,16 +513,16 @@ int stream_max_resident_blocks(int W, int *per_cu, int *cus)
         return -3;
     const void *fn = nullptr;
     switch (W) {
-    case 8: fn = (const void *)stream_kernel<8, 4>; break;
-    case 16: fn = (const void *)stream_kernel<16, 8>; break;
-    case 32: fn = (const void *)stream_kernel<32, 8>; break;
-    case 64: fn = (const void *)stream_kernel<64, 8>; break;
-    case 128: fn = (const void *)stream_kernel<128, 8>; break;
-    case 256: fn = (const void *)stream_kernel<256, 8>; break;
-    case 512: fn = (const void *)stream_kernel<512, 8>; break;
-    case 1024: fn = (const void *)stream_kernel<1024, 8>; break;
-    case 2048: fn = (const void *)stream_kernel<2048, 8>; break;
-    case 4096: fn = (const void *)stream_kernel<4096, 8>; break;
+    case 8: fn = (const void *)stream_kernel<8, 4, 4>; break;
+    case 16: fn = (const void *)stream_kernel<16, 8, 4>; break;
+    case 32: fn = (const void *)stream_kernel<32, 8, 4>; break;
+    case 64: fn = (const void *)stream_kernel<64, 8, 4>; break;
+    case 128: fn = (const void *)stream_kernel<128, 8, 4>; break;
+    case 256: fn = (const void *)stream_kernel<256, 8, 4>; break;
+    case 512: fn = (const void *)stream_kernel<512, 8, 4>; break;
+    case 1024: fn = (const void *)stream_kernel<1024, 8, 4>; break;
+    case 2048: fn = (const void *)stream_kernel<2048, 8, 4>; break;
+    case 4096: fn = (const void *)stream_kernel<4096, 8, 4>; break;
     default: return -1;
     }
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 256, 0) != hipSuccess) return -3;

@@ -79,6 +79,7 @@ typedef struct burg_stats {
     int64_t stall_spins;        /* streaming engine: polls of not-yet-ready edge data */
     int64_t slow_diagonals;     /* streaming engine: diagonals that took the slow path */
     int64_t stream_launches;    /* streaming engine: launches (one per run chunk) */
+    int64_t slow_ticks;         /* streaming engine: shader clocks spent on the slow path */
 } burg_stats;
 
 enum burg_engine {

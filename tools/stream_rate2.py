@@ -5,7 +5,9 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from finitedifference_amd.solver import FOMContext
 nx = ny = 1024
-for flags in ("0", "1", "2", "3"):
+for flags in ("8",):
+  for R in ("8", "32", "128"):
+    os.environ["BURG_STREAM_R"] = R
     os.environ["BURG_STREAM_DEBUG"] = flags
     for W in (16, 32):
         c = FOMContext(nx, ny, stream_w=W)
@@ -15,5 +17,5 @@ for flags in ("0", "1", "2", "3"):
         t1 = c.advance(50)["loop_ms"]
         st = c.advance(550)
         t2 = st["loop_ms"]
-        print(f"flags={flags} W={W} per-diag {(t2-t1)*1e6/(500*W):.0f} ns  t550 {t2:.3f} ms  "
-              f"spins {st['stall_spins']}", flush=True)
+        print(f"R={R} flags={flags} W={W} per-diag {(t2-t1)*1e6/(500*W):.0f} ns  t550 {t2:.3f} ms  "
+              f"spins {st['stall_spins']} slow {st['slow_diagonals']} slow_ms/wave {st['slow_ticks']/max(1,st['stream_tiles'])/2.1e6:.3f}", flush=True)
