@@ -13,19 +13,19 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
-BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_ERCCL = 0, -1, -2, -3, -4
+BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
 SOLVERS = {"march": 0, "newton": 1}
-ENGINES = {"stream": 0, "tiles": 1}
+ENGINES = {"stream": 0, "tiles": 1, "pipe": 2}
 
 # Every symbol include/burgers.h declares (checked by tests/test_capi.py).
 EXPORTS = (
-    "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_rccl_unique_id",
-    "burg_ctx_create_slab", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
+    "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_ctx_create_slab",
+    "burg_slab_connect", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
-    "burg_advance", "burg_download_state", "burg_set_engine",
+    "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
 )
 
 
@@ -53,6 +53,8 @@ class BurgStats(ctypes.Structure):
         ("slow_diagonals", ctypes.c_int64),
         ("stream_launches", ctypes.c_int64),
         ("slow_ticks", ctypes.c_int64),
+        ("ieee_diagonals", ctypes.c_int64),
+        ("comm_polls", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -94,8 +96,9 @@ def load(path=None):
             "burg_last_error": (ctypes.c_char_p, []),
             "burg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.POINTER(_VP)]),
-            "burg_rccl_unique_id": (ctypes.c_int, [_VP]),
-            "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [_VP, ctypes.POINTER(_VP)]),
+            "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.c_char_p,
+                                                                         ctypes.POINTER(_VP)]),
+            "burg_slab_connect": (ctypes.c_int, [_VP]),
             "burg_ctx_destroy": (None, [_VP]),
             "burg_set_problem": (ctypes.c_int, [_VP, _D, _D, _D, _D, ctypes.c_double]),
             "burg_set_options": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
@@ -110,6 +113,8 @@ def load(path=None):
             "burg_advance": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                             ctypes.POINTER(BurgStats)]),
             "burg_download_state": (ctypes.c_int, [_VP, _D]),
+            "burg_trajectory": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
+                                                ctypes.POINTER(BurgStats)]),
             "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
         }
         for name, (res, args) in sig.items():

@@ -100,6 +100,35 @@ struct StreamArgs {
     StreamStats *stats;
 };
 
+// ---- pipe engine (pipe.hip) ---------------------------
+// Same tiles and ring as the streaming engine; a workgroup holds 4 adjacent
+// tiles of one strip (4 compute waves) plus one comm wave.  Global mailboxes
+// use two sentinel colours so that a slot's emptiness is tied to a step.
+constexpr int kPipeR = 8;   // global mailbox slots (steps) per edge, power of two
+constexpr int kPipeRL = 4;  // LDS ring slots (steps) per intra-workgroup edge
+
+struct PipeArgs {
+    Coeffs cf;
+    const d2 *colc;       // [ntj*W] {hx, src}
+    d2 *ring;             // [ntiles][L][64]
+    d2 *wbox;             // [ntiles][kPipeR][64] granules (kGranuleStride apart)
+    d2 *sbox;             // [ntiles][kPipeR][W]
+    size_t wbox_bytes, sbox_bytes;
+    // Multi-GPU halo rings in pinned host memory shared with the neighbour
+    // ranks (system scope): [kPipeR][ntj*W] granules, 16 B apart.  nullptr:
+    // no neighbour on that side (domain boundary).
+    d2 *halo_in;          // south inflow of the bottom strip (written by rank-1)
+    d2 *halo_out;         // north outflow of the top strip (read by rank+1)
+    size_t halo_bytes;
+    long long origin, L;  // ring entry of diagonal 0, ring length
+    int K;                // steps of this launch
+    int qbase;            // absolute step of local step 0, mod 2*kPipeR (sentinel colour)
+    int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
+    long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
+    unsigned *err;        // [4]: flag, tile, diagonal/step, which wait
+    StreamStats *stats;
+};
+
 }  // namespace burg
 
 // ---- host-side launch wrappers (defined in the .hip files) ----------------
@@ -128,6 +157,10 @@ int launch_fill_sentinel(void *p, size_t n16, hipStream_t st);
 int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st);
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
                         int ldo, hipStream_t st);
+bool pipe_width_supported(int W);
+int pipe_max_resident_blocks(int W);
+int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
+int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
                      int ldo, hipStream_t st);
 

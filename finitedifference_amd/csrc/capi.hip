@@ -12,6 +12,10 @@
 #include <string>
 #include <vector>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include "../../include/burgers.h"
 #include "burg_internal.h"
 
@@ -97,6 +101,7 @@ struct burg_ctx {
     // states (ping-pong) and scratch
     double *d_state[2] = {nullptr, nullptr};
     int cur = 0;
+    double *d_w0 = nullptr;  // last uploaded state (burg_trajectory from_initial)
     double *d_r = nullptr, *d_d = nullptr, *d_x = nullptr, *d_partials = nullptr,
            *d_sumsq = nullptr;
     int npartials = 0;
@@ -111,6 +116,17 @@ struct burg_ctx {
     size_t box16 = 0, ring_entries = 0;
     unsigned *d_err = nullptr;
     StreamStats *d_sstats = nullptr;
+    // pipe engine (pipe.hip): effective engine of march runs, workgroups per
+    // strip, absolute step counter mod 2*kPipeR (mailbox sentinel colour)
+    int eng_eff = BURG_ENGINE_STREAM;
+    int nwj = 0, qbase = 0;
+    long long spin_ticks = 500000000LL;  // 5 s of s_memrealtime (100 MHz)
+    // multi-GPU halo rings (pinned shared host memory)
+    std::string halo_name;
+    void *halo_in_host = nullptr, *halo_out_host = nullptr;
+    d2 *halo_in_dev = nullptr, *halo_out_dev = nullptr;
+    size_t halo_bytes = 0;
+    bool halo_connected = false;
 
     size_t m() const { return 2 * (size_t)nx * nrows; }
     size_t n() const { return (size_t)nx * nrows; }
@@ -293,40 +309,97 @@ void stream_free(burg_ctx *c)
     c->sp_ready = c->colc_ready = false;
 }
 
+// Pipe engine plan: W in {8, 16} (the narrowest whose tile count fits the
+// target), every workgroup (4 tiles + comm wave) resident at once.
+bool pipe_plan(burg_ctx *c, int target, StreamPlan *out, int *nwj)
+{
+    int Ws[2] = {8, 16};
+    int n = 2;
+    if (c->stream_w_opt != 0) {
+        if (!pipe_width_supported(c->stream_w_opt)) return false;
+        Ws[0] = c->stream_w_opt;
+        n = 1;
+    }
+    for (int i = 0; i < n; ++i) {
+        const int W = Ws[i];
+        StreamPlan p = plan_stream(c->nx, c->nrows, 0, W);
+        const int wj = (p.ntj + 3) / 4;
+        const int cap = pipe_max_resident_blocks(W);
+        if (cap < 0) return false;
+        const bool last = i + 1 == n;
+        if (p.nti * wj <= cap && (p.ntiles <= target || last)) {
+            p.R = kPipeR;
+            *out = p;
+            *nwj = wj;
+            return true;
+        }
+    }
+    return false;
+}
+
 // Plan the tiling (capped by residency: every tile's wavefront must be live
 // at once), allocate the mailboxes (all sentinel) and the column table.
 int stream_setup(burg_ctx *c)
 {
     if (!c->sp_ready) {
         const int target = c->tiles_target_opt > 0 ? c->tiles_target_opt : 1024;
-        StreamPlan p = plan_stream(c->nx, c->nrows, target, c->stream_w_opt);
-        for (;;) {
-            if (!stream_width_supported(p.W))
-                return fail(BURG_EINVAL, "stream tile width %d not supported (8..4096, power of 2)",
-                            p.W);
-            int per_cu = 0, cus = 0;
-            const int cap = stream_max_resident_blocks(p.W, &per_cu, &cus);
-            if (cap < 0) return fail(BURG_EHIP, "occupancy query failed");
-            if (p.ntiles <= 4 * cap) break;
-            if (c->stream_w_opt > 0 || p.W >= 4096)
-                return fail(BURG_ESHAPE, "%d tiles of width %d exceed the %d resident wavefronts",
-                            p.ntiles, p.W, 4 * cap);
-            p = plan_stream(c->nx, c->nrows, 0, p.W * 2);
+        StreamPlan pp{};
+        int wj = 0;
+        if (c->engine == BURG_ENGINE_PIPE && pipe_plan(c, target, &pp, &wj)) {
+            c->sp = pp;
+            c->nwj = wj;
+            c->eng_eff = BURG_ENGINE_PIPE;
+            c->box16 = (size_t)pp.ntiles * kPipeR * (kWave + pp.W) * (kGranuleStride / sizeof(d2));
+            if (c->box16 * sizeof(d2) >= (1ull << 31))
+                return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB");
+            if (int e = dalloc(&c->d_boxes, c->box16)) return e;
+            if (int e = dalloc(&c->d_colc, (size_t)pp.ntj * pp.W)) return e;
+            if (int e = dalloc(&c->d_err, 4)) return e;
+            if (int e = dalloc(&c->d_sstats, 1)) return e;
+            CHK(launch_pipe_fill(c->d_boxes, c->box16, 0, c->stream));
+            HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
+            c->qbase = 0;
+            c->sp_ready = true;
+            c->colc_ready = false;
+        } else {
+            if (c->world > 1)
+                return fail(BURG_ESHAPE,
+                            "multi-GPU slabs need the pipe engine: a %d-row x %d slab does not fit "
+                            "one resident workgroup per 4 tiles of width 8 or 16",
+                            c->nrows, c->nx);
+            StreamPlan p = plan_stream(c->nx, c->nrows, target,
+                                       c->engine == BURG_ENGINE_PIPE ? 0 : c->stream_w_opt);
+            for (;;) {
+                if (!stream_width_supported(p.W))
+                    return fail(BURG_EINVAL, "stream tile width %d not supported (8..4096, power of 2)",
+                                p.W);
+                int per_cu = 0, cus = 0;
+                const int cap = stream_max_resident_blocks(p.W, &per_cu, &cus);
+                if (cap < 0) return fail(BURG_EHIP, "occupancy query failed");
+                if (p.ntiles <= 4 * cap) break;
+                if ((c->engine == BURG_ENGINE_STREAM && c->stream_w_opt > 0) || p.W >= 4096)
+                    return fail(BURG_ESHAPE, "%d tiles of width %d exceed the %d resident wavefronts",
+                                p.ntiles, p.W, 4 * cap);
+                p = plan_stream(c->nx, c->nrows, 0, p.W * 2);
+            }
+            c->sp = p;
+            c->eng_eff = BURG_ENGINE_STREAM;
+            c->box16 = (size_t)p.ntiles * p.R * (kWave + p.W) * (kGranuleStride / sizeof(d2));
+            if (c->box16 * sizeof(d2) >= (1ull << 31))
+                return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB (%d tiles of width %d)",
+                            p.ntiles, p.W);
+            if (int e = dalloc(&c->d_boxes, c->box16)) return e;
+            if (int e = dalloc(&c->d_colc, (size_t)p.ntj * p.W)) return e;
+            if (int e = dalloc(&c->d_err, 4)) return e;
+            if (int e = dalloc(&c->d_sstats, 1)) return e;
+            CHK(launch_fill_sentinel(c->d_boxes, c->box16, c->stream));
+            HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
+            c->sp_ready = true;
+            c->colc_ready = false;
         }
-        c->sp = p;
-        c->box16 = (size_t)p.ntiles * p.R * (kWave + p.W) * (kGranuleStride / sizeof(d2));
-        if (c->box16 * sizeof(d2) >= (1ull << 31))
-            return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB (%d tiles of width %d)",
-                        p.ntiles, p.W);
-        if (int e = dalloc(&c->d_boxes, c->box16)) return e;
-        if (int e = dalloc(&c->d_colc, (size_t)p.ntj * p.W)) return e;
-        if (int e = dalloc(&c->d_err, 4)) return e;
-        if (int e = dalloc(&c->d_sstats, 1)) return e;
-        CHK(launch_fill_sentinel(c->d_boxes, c->box16, c->stream));
-        HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
-        c->sp_ready = true;
-        c->colc_ready = false;
     }
+    if (c->world > 1 && !c->halo_connected)
+        return fail(BURG_ESTATE, "slab context not connected (burg_slab_connect) to its neighbours");
     if (!c->colc_ready) {
         CHK(launch_colc(c->cf, c->sp.ntj * c->sp.W, c->d_colc, c->stream));
         c->colc_ready = true;
@@ -371,11 +444,42 @@ StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
 // max steps per launch so that K*W stays an int
 int stream_max_steps(const burg_ctx *c) { return (1 << 29) / c->sp.W; }
 
+PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
+{
+    PipeArgs a{};
+    a.cf = c->cf;
+    a.colc = c->d_colc;
+    a.ring = c->d_ring;
+    a.wbox = c->d_boxes;
+    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * kPipeR * kWave * (kGranuleStride / sizeof(d2));
+    a.wbox_bytes = (size_t)c->sp.ntiles * kPipeR * kWave * kGranuleStride;
+    a.sbox_bytes = (size_t)c->sp.ntiles * kPipeR * c->sp.W * kGranuleStride;
+    a.halo_in = c->halo_in_dev;
+    a.halo_out = c->halo_out_dev;
+    a.halo_bytes = c->halo_bytes;
+    a.origin = origin;
+    a.L = L;
+    a.K = K;
+    a.qbase = c->qbase;
+    a.nti = c->sp.nti;
+    a.ntj = c->sp.ntj;
+    a.ntiles = c->sp.ntiles;
+    a.nwj = c->nwj;
+    a.spin_ticks = c->spin_ticks;
+    a.err = c->d_err;
+    a.stats = c->d_sstats;
+    return a;
+}
+
 int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
 {
-    const StreamArgs a = stream_args(c, L, origin, K);
+    const bool pipe = c->eng_eff == BURG_ENGINE_PIPE;
     HIPCHK(hipEventRecord(c->ev0, c->stream));
-    CHK(launch_stream(a, c->sp.W, c->stream));
+    if (pipe) {
+        CHK(launch_pipe(pipe_args(c, L, origin, K), c->sp.W, c->stream));
+    } else {
+        CHK(launch_stream(stream_args(c, L, origin, K), c->sp.W, c->stream));
+    }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
     HIPCHK(hipEventSynchronize(c->ev1));
     float t = 0.f;
@@ -386,13 +490,26 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
     if (err[0]) {
         // leave the mailboxes clean for the next launch
         (void)hipMemsetAsync(c->d_err, 0, sizeof err, c->stream);
-        (void)launch_fill_sentinel(c->d_boxes, c->box16, c->stream);
+        if (pipe) {
+            (void)launch_pipe_fill(c->d_boxes, c->box16, 0, c->stream);
+            c->qbase = 0;
+        } else {
+            (void)launch_fill_sentinel(c->d_boxes, c->box16, c->stream);
+        }
         (void)hipStreamSynchronize(c->stream);
+        if (pipe)
+            return fail(BURG_EHIP,
+                        "pipe engine: a wait timed out (workgroup tile %u of %d, step/diagonal %u, "
+                        "wait %#x [16: comm wave: 1 south 2 west 4 north-grant 8 east-grant; 32: "
+                        "compute wave], K=%d W=%d%s)",
+                        err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W,
+                        c->world > 1 ? "; multi-GPU: a neighbour rank may not be running" : "");
         return fail(BURG_EHIP,
                     "streaming engine: an edge wait timed out (tile %u of %d, diagonal %u, "
                     "edges %u [1 west 2 south 4 east 8 north], K=%d W=%d)",
                     err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W);
     }
+    if (pipe) c->qbase = (int)((c->qbase + (long long)K) % (2 * kPipeR));
     return 0;
 }
 
@@ -412,7 +529,7 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->passes = steps;
         st->max_passes = steps > 0 ? 1 : 0;
         st->unconverged_steps = 0;
-        st->engine = BURG_ENGINE_STREAM;
+        st->engine = c->eng_eff;
         st->stream_w = c->sp.W;
         st->stream_tiles = c->sp.ntiles;
         st->stall_spins = (int64_t)ss.stall_spins;
@@ -425,6 +542,8 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
                              ss.why[0], ss.why[1], ss.why[2], ss.why[3], ss.why[4], ss.why[5]);
         st->slow_ticks = (int64_t)ss.slow_ticks;
         st->stream_launches = launches;
+        st->ieee_diagonals = (int64_t)ss.ieee_diagonals;
+        st->comm_polls = c->eng_eff == BURG_ENGINE_PIPE ? (int64_t)ss.why[5] : 0;
     }
     return 0;
 }
@@ -464,6 +583,38 @@ int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
             st->march_kernel_ms = ms;
             st->march_launches = launches;
         }
+    }
+    return 0;
+}
+
+// One device-resident trajectory: num_steps steps from d_state[cur] in ONE
+// launch, every state kept in the ring (HBM) -- the reference's snapshot
+// matrix in ring layout (C/hypernet2D.py:89-126 keeps them all); the final
+// state becomes d_state[cur].
+int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats *st)
+{
+    if (int e = stream_setup(c)) return e;
+    if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
+    if (num_steps > stream_max_steps(c))
+        return fail(BURG_EINVAL, "num_steps %d exceeds one launch (%d)", num_steps,
+                    stream_max_steps(c));
+    const int W = c->sp.W;
+    const long long L = (long long)num_steps * W + W + 96;
+    if (int e = ensure_ring(c, L)) return e;
+    if (from_initial && !c->d_w0) return fail(BURG_ESTATE, "no uploaded initial state");
+    stream_stats_begin(c);
+    CHK(launch_ring_load(stream_args(c, L, 0, 0), W, from_initial ? c->d_w0 : c->d_state[c->cur],
+                         c->stream));
+    float ms = 0.f;
+    if (int e = stream_launch(c, L, 0, num_steps, &ms)) return e;
+    CHK(launch_ring_extract(stream_args(c, L, 0, 0), W, num_steps, 1, 1, c->d_state[c->cur ^ 1],
+                            1, c->stream));
+    c->cur ^= 1;
+    if (int e = stream_stats_end(c, st, num_steps, 1)) return e;
+    if (st) {
+        st->loop_ms = ms;
+        st->march_kernel_ms = ms;
+        st->march_launches = 1;
     }
     return 0;
 }
@@ -587,6 +738,66 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
     return rc;
 }
 
+// ---- multi-GPU halo rings ------------------------------------------------
+// One ring per rank boundary b (between ranks b-1 and b): kPipeR step slots x
+// nx granules of 16 B in POSIX shared memory, created and initialised (all
+// slots: sentinel colour 0) by the consumer rank b, attached by the producer
+// rank b-1, pinned and mapped into each GPU's address space.  Both GPUs reach
+// it at system scope; no host thread touches it at run time.
+std::string halo_shm_name(const std::string &job, int boundary)
+{
+    return "/burg_" + job + "_b" + std::to_string(boundary);
+}
+
+int halo_map(burg_ctx *c, const std::string &name, bool create, void **host, d2 **dev)
+{
+    const size_t bytes = c->halo_bytes;
+    const int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+    if (fd < 0) return fail(BURG_EHALO, "shm_open(%s): %s", name.c_str(), strerror(errno));
+    if (create && ftruncate(fd, (off_t)bytes) != 0) {
+        close(fd);
+        shm_unlink(name.c_str());
+        return fail(BURG_EHALO, "ftruncate(%s): %s", name.c_str(), strerror(errno));
+    }
+    void *p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return fail(BURG_EHALO, "mmap(%s): %s", name.c_str(), strerror(errno));
+    if (create) {
+        // sentinel colour 0 (pipe.hip): {lo 0xBEEF5A5A, hi 0x7FF4DEAD} in both halves
+        uint32_t *w = (uint32_t *)p;
+        for (size_t i = 0; i < bytes / 4; i += 2) {
+            w[i] = 0xBEEF5A5Au;
+            w[i + 1] = 0x7FF4DEADu;
+        }
+    }
+    hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
+    if (e != hipSuccess) {
+        munmap(p, bytes);
+        return fail(BURG_EHALO, "hipHostRegister(%s, %zu): %s", name.c_str(), bytes,
+                    hipGetErrorString(e));
+    }
+    void *dp = nullptr;
+    e = hipHostGetDevicePointer(&dp, p, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(p);
+        munmap(p, bytes);
+        return fail(BURG_EHALO, "hipHostGetDevicePointer(%s): %s", name.c_str(), hipGetErrorString(e));
+    }
+    *host = p;
+    *dev = (d2 *)dp;
+    return 0;
+}
+
+void halo_unmap(burg_ctx *c, void *&host, d2 *&dev)
+{
+    if (host) {
+        (void)hipHostUnregister(host);
+        munmap(host, c->halo_bytes);
+    }
+    host = nullptr;
+    dev = nullptr;
+}
+
 }  // namespace
 
 extern "C" {
@@ -600,23 +811,25 @@ int burg_ctx_create(int device, int nx, int ny, burg_ctx **out)
     return burg_ctx_create_slab(device, nx, ny, 0, ny, 0, 1, nullptr, out);
 }
 
-int burg_rccl_unique_id(void *id_out)
-{
-    if (!id_out) return fail(BURG_EINVAL, "null id buffer");
-    return fail(BURG_ERCCL, "multi-GPU slabs are not built into this library yet");
-}
-
 int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, int rank,
-                         int world, const void *nccl_id, burg_ctx **out)
+                         int world, const char *halo_name, burg_ctx **out)
 {
     if (!out) return fail(BURG_EINVAL, "null out pointer");
     *out = nullptr;
     if (nx < 1 || ny_total < 1 || row0 < 0 || nrows < 1 || row0 + nrows > ny_total)
         return fail(BURG_EINVAL, "bad grid: nx=%d ny=%d row0=%d nrows=%d", nx, ny_total, row0,
                     nrows);
-    if (world != 1 || rank != 0 || row0 != 0 || nrows != ny_total)
-        return fail(BURG_ERCCL, "multi-GPU slabs are not built into this library yet");
-    (void)nccl_id;
+    if (world < 1 || rank < 0 || rank >= world)
+        return fail(BURG_EINVAL, "bad rank %d of world %d", rank, world);
+    if (world == 1 && (row0 != 0 || nrows != ny_total))
+        return fail(BURG_EINVAL, "a single-rank context owns the whole grid");
+    if (world > 1) {
+        if (!halo_name || !*halo_name || std::strlen(halo_name) > 64 ||
+            std::strchr(halo_name, '/'))
+            return fail(BURG_EINVAL, "multi-GPU slabs need a halo name (1-64 chars, no '/')");
+        if ((rank == 0) != (row0 == 0) || (rank == world - 1) != (row0 + nrows == ny_total))
+            return fail(BURG_EINVAL, "rank %d of %d does not own its slab's end rows", rank, world);
+    }
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev)
@@ -630,6 +843,11 @@ int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, 
     c->nrows = nrows;
     c->rank = rank;
     c->world = world;
+    c->engine = BURG_ENGINE_PIPE;
+    if (const char *e = std::getenv("BURG_SPIN_SECONDS")) {
+        const double v = std::atof(e);
+        if (v > 0) c->spin_ticks = (long long)(v * 1e8);
+    }
     int e = 0;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
@@ -647,7 +865,33 @@ int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, 
         burg_ctx_destroy(c);
         return e;
     }
+    if (world > 1) {
+        c->halo_name = halo_name;
+        c->halo_bytes = (size_t)kPipeR * nx * sizeof(d2);
+        if (rank > 0) {
+            const std::string nm = halo_shm_name(c->halo_name, rank);
+            if ((e = halo_map(c, nm, true, &c->halo_in_host, &c->halo_in_dev))) {
+                burg_ctx_destroy(c);
+                return e;
+            }
+        }
+    } else {
+        c->halo_connected = true;
+    }
     *out = c;
+    return BURG_OK;
+}
+
+int burg_slab_connect(burg_ctx *c)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (c->world == 1 || c->halo_connected) return BURG_OK;
+    HIPCHK(hipSetDevice(c->device));
+    if (c->rank + 1 < c->world) {
+        const std::string nm = halo_shm_name(c->halo_name, c->rank + 1);
+        if (int e = halo_map(c, nm, false, &c->halo_out_host, &c->halo_out_dev)) return e;
+    }
+    c->halo_connected = true;
     return BURG_OK;
 }
 
@@ -667,12 +911,16 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_stats_solve);
     dfree(c->d_state[0]);
     dfree(c->d_state[1]);
+    dfree(c->d_w0);
     dfree(c->d_r);
     dfree(c->d_d);
     dfree(c->d_x);
     dfree(c->d_partials);
     dfree(c->d_sumsq);
     stream_free(c);
+    halo_unmap(c, c->halo_in_host, c->halo_in_dev);
+    halo_unmap(c, c->halo_out_host, c->halo_out_dev);
+    if (c->world > 1 && c->rank > 0) shm_unlink(halo_shm_name(c->halo_name, c->rank).c_str());
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -731,15 +979,18 @@ int burg_set_options(burg_ctx *c, int tile_w, int par_passes, double tol, int pr
 int burg_set_engine(burg_ctx *c, int engine, int stream_w, int tiles_target)
 {
     if (!c) return fail(BURG_EINVAL, "null context");
-    if (engine != BURG_ENGINE_STREAM && engine != BURG_ENGINE_TILES)
+    if (engine != BURG_ENGINE_STREAM && engine != BURG_ENGINE_TILES && engine != BURG_ENGINE_PIPE)
         return fail(BURG_EINVAL, "unknown engine %d", engine);
+    if (c->world > 1 && engine != BURG_ENGINE_PIPE)
+        return fail(BURG_EINVAL, "multi-GPU slabs run on the pipe engine only");
     if (stream_w != 0 && !stream_width_supported(stream_w))
         return fail(BURG_EINVAL, "stream_w must be 0 or a power of two in [8, 4096]");
     if (tiles_target < 0) return fail(BURG_EINVAL, "tiles_target < 0");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
+    const bool replan = engine != c->engine;
     c->engine = engine;
-    if (stream_w != c->stream_w_opt || tiles_target != c->tiles_target_opt) {
+    if (replan || stream_w != c->stream_w_opt || tiles_target != c->tiles_target_opt) {
         stream_free(c);
         c->stream_w_opt = stream_w;
         c->tiles_target_opt = tiles_target;
@@ -797,6 +1048,10 @@ int burg_upload_state(burg_ctx *c, const double *w)
     if (!w) return fail(BURG_EINVAL, "null state");
     HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w, c->m() * sizeof(double),
                           hipMemcpyHostToDevice, c->stream));
+    if (!c->d_w0)
+        if (int e = dalloc(&c->d_w0, c->m())) return e;
+    HIPCHK(hipMemcpyAsync(c->d_w0, c->d_state[c->cur], c->m() * sizeof(double),
+                          hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BURG_OK;
 }
@@ -818,7 +1073,7 @@ int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
     if (solver != BURG_SOLVER_MARCH && solver != BURG_SOLVER_NEWTON)
         return fail(BURG_EINVAL, "unknown solver %d", solver);
     if (st) std::memset(st, 0, sizeof *st);
-    if (solver == BURG_SOLVER_MARCH && c->engine == BURG_ENGINE_STREAM)
+    if (solver == BURG_SOLVER_MARCH && c->engine != BURG_ENGINE_TILES)
         return stream_advance(c, num_steps, st);
     HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream));
     if (solver == BURG_SOLVER_NEWTON)
@@ -856,6 +1111,15 @@ int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
     return BURG_OK;
 }
 
+int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (st) std::memset(st, 0, sizeof *st);
+    if (c->engine == BURG_ENGINE_TILES)
+        return fail(BURG_EINVAL, "burg_trajectory runs on the stream/pipe engines");
+    return stream_trajectory(c, num_steps, from_initial != 0, st);
+}
+
 int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newton_max_its,
              double newton_rtol, double *snaps, int64_t ld_snaps, int snap_every,
              burg_stats *st, int32_t *step_iters, double *step_rel)
@@ -872,7 +1136,7 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
                     (long long)ncols);
     if (newton_max_its < 0) return fail(BURG_EINVAL, "newton_max_its < 0");
     if (st) std::memset(st, 0, sizeof *st);
-    if (solver == BURG_SOLVER_MARCH && c->engine == BURG_ENGINE_STREAM)
+    if (solver == BURG_SOLVER_MARCH && c->engine != BURG_ENGINE_TILES)
         return stream_run(c, w0, num_steps, snaps, ld_snaps, snap_every, st, step_iters,
                           step_rel);
     if (int e = ensure_scratch(c)) return e;

@@ -129,9 +129,12 @@ struct MarchCell {
         const double q = 0.25 + mm;
         double s, nu, nv;
         if constexpr (FAST) {
-            // (NaN in cu or cv fails too: the streaming engine relies on it)
-            range_ok = fmin(fabs(cu), fabs(cv)) >= 0x1p-900 && fabs(cu) <= 0x1p+900 &&
-                       fabs(cv) <= 0x1p+900;
+            // operands +0 or of magnitude in [2^-900, 2^900]: div2_normal's exact
+            // range (-0 would come out +0; NaN fails too: the streaming engines
+            // rely on it)
+            const double au = fabs(cu), av = fabs(cv);
+            range_ok = ((au >= 0x1p-900 && au <= 0x1p+900) || __double_as_longlong(cu) == 0) &&
+                       ((av >= 0x1p-900 && av <= 0x1p+900) || __double_as_longlong(cv) == 0);
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

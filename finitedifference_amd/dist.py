@@ -1,11 +1,22 @@
-"""Row-slab decomposition over GPUs (one process per GPU, RCCL over xGMI).
+"""Row-slab decomposition over GPUs (one process per GPU).
 
 Rank k owns the contiguous global rows [row0_k, row0_k + rows_k) of the
 nx x ny grid (rows split as evenly as possible, remainder to the first
-ranks, e.g. 750 over 8 = 94,94,94,94,94,94,93,93).  The upwind march couples
-a slab only to the row just below it, so the exchange is one-way
-(rank k -> k+1) and happens inside libburgers_hip over RCCL.
+ranks, e.g. 750 over 8 = 94,94,94,94,94,94,93,93; rank 0 is the bottom slab,
+y = 0).  The upwind march couples a slab only to the row just below it
+(C/hypernet2D.py:2410-2416: backward differences), so the exchange is
+one-way, rank k -> k+1: the north outflow of rank k's top row is the south
+inflow of rank k+1's bottom row.  Inside libburgers_hip that stream runs
+GPU-to-GPU through a ring in shared pinned host memory while both time loops
+are running; this module only agrees on the ring's
+name, orders context creation around a barrier, and splits / assembles
+states and snapshot matrices in the reference layout.
 """
+import os
+import secrets
+
+import numpy as np
+
 from .solver import FOMContext
 
 
@@ -16,7 +27,60 @@ def slab_rows(ny, world, rank):
     return row0, rows
 
 
-def make_slab_context(nx, ny, rank=0, world=1, device=0, **opts):
+def slab_state(w, nx, ny, rank, world):
+    """This rank's part of a global state w = [u.ravel(), v.ravel()] (u
+    row-major (ny, nx), C/run_fom.py:33-35): [u rows | v rows] of the slab."""
+    w = np.asarray(w, dtype=np.float64).reshape(2, ny, nx)
+    row0, rows = slab_rows(ny, world, rank)
+    return np.ascontiguousarray(w[:, row0:row0 + rows, :]).ravel()
+
+
+def assemble_state(parts, nx, ny):
+    """Inverse of slab_state over all ranks (parts in rank order)."""
+    world = len(parts)
+    out = np.empty((2, ny, nx))
+    for r, p in enumerate(parts):
+        row0, rows = slab_rows(ny, world, r)
+        out[:, row0:row0 + rows, :] = np.asarray(p).reshape(2, rows, nx)
+    return out.ravel()
+
+
+def assemble_snaps(parts, nx, ny):
+    """Global snapshot matrix (2*nx*ny, ncols), the reference's layout, from
+    per-rank slab snapshot matrices (2*nx*rows_k, ncols)."""
+    world = len(parts)
+    ncols = parts[0].shape[1]
+    out = np.empty((2, ny, nx, ncols))
+    for r, p in enumerate(parts):
+        row0, rows = slab_rows(ny, world, r)
+        out[:, row0:row0 + rows] = np.asarray(p).reshape(2, rows, nx, ncols)
+    return out.reshape(2 * ny * nx, ncols)
+
+
+def agree_halo_name(dist=None):
+    """A job-unique ring name, made by rank 0 and broadcast (torch.distributed,
+    any backend).  Without a process group: a fresh name (single process)."""
+    name = f"{os.getpid():x}{secrets.token_hex(6)}"
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        box = [name]
+        dist.broadcast_object_list(box, src=0)
+        name = box[0]
+    return name
+
+
+def make_slab_context(nx, ny, rank=0, world=1, device=0, dist=None, halo_name=None, **opts):
+    """Context for rank `rank`'s slab.  world > 1: every rank must call this
+    together (it creates this rank's inbound halo ring, waits on a barrier
+    until all rings exist, then attaches the outbound one)."""
     if world == 1:
         return FOMContext(nx, ny, device, **opts)
-    return FOMContext.slab(nx, ny, rank, world, device, **opts)
+    if dist is None:
+        import torch.distributed as dist
+    if halo_name is None:
+        halo_name = agree_halo_name(dist)
+    row0, rows = slab_rows(ny, world, rank)
+    ctx = FOMContext.slab(nx, ny, row0, rows, rank, world, halo_name, device, **opts)
+    dist.barrier()
+    ctx.connect()
+    dist.barrier()
+    return ctx

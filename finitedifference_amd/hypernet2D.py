@@ -65,7 +65,7 @@ def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
 
 
 def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
-                                snap_every=1, device=0, engine="stream", tile_w=64,
+                                snap_every=1, device=0, engine="pipe", tile_w=64,
                                 tol=DEFAULT_TOL, par_passes=0, verbose=1, allow_nonsquare=False,
                                 newton_max_its=100, newton_rtol=1e-12, return_stats=False):
     """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM

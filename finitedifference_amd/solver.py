@@ -20,15 +20,32 @@ class FOMContext:
     """A grid (nx x ny) resident on one GPU."""
 
     def __init__(self, nx, ny, device=0, tile_w=64, par_passes=0, tol=DEFAULT_TOL,
-                 profile=False, engine="stream", stream_w=0, tiles_target=0):
+                 profile=False, engine="pipe", stream_w=0, tiles_target=0, _slab=None):
         self._L = _lib.load()
         self.nx, self.ny, self.device = int(nx), int(ny), int(device)
         h = ctypes.c_void_p()
-        _lib.check(self._L.burg_ctx_create(self.device, self.nx, self.ny, ctypes.byref(h)))
+        if _slab is None:
+            self.ny_total, self.row0, self.rank, self.world = self.ny, 0, 0, 1
+            _lib.check(self._L.burg_ctx_create(self.device, self.nx, self.ny, ctypes.byref(h)))
+        else:
+            self.ny_total, self.row0, self.rank, self.world, name = _slab
+            _lib.check(self._L.burg_ctx_create_slab(self.device, self.nx, self.ny_total, self.row0,
+                                                    self.ny, self.rank, self.world,
+                                                    name.encode(), ctypes.byref(h)))
         self._h = h
         self._problem = None
         self.set_options(tile_w, par_passes, tol, profile)
         self.set_engine(engine, stream_w, tiles_target)
+
+    @classmethod
+    def slab(cls, nx, ny_total, row0, rows, rank, world, halo_name, device=0, **opts):
+        """Rank `rank`'s slab (global rows [row0, row0+rows)) of an nx x ny_total
+        grid; call connect() once every rank has created its slab context."""
+        return cls(nx, rows, device, _slab=(int(ny_total), int(row0), int(rank), int(world),
+                                            str(halo_name)), **opts)
+
+    def connect(self):
+        _lib.check(self._L.burg_slab_connect(self._h))
 
     @property
     def m(self):
@@ -50,21 +67,24 @@ class FOMContext:
                                             1 if profile else 0))
         self.options = dict(tile_w=tile_w, par_passes=par_passes, tol=tol, profile=profile)
 
-    def set_engine(self, engine="stream", stream_w=0, tiles_target=0):
-        """March engine: "stream" (exact pipelined march, one launch per run
-        chunk; the default) or "tiles" (block-Jacobi tile passes per step,
-        tuned by set_options)."""
+    def set_engine(self, engine="pipe", stream_w=0, tiles_target=0):
+        """March engine: "pipe" (the default: exact pipelined march, one launch
+        per run chunk, LDS edges and a comm wave per workgroup; falls back to
+        "stream" on one GPU when the grid needs tiles wider than 16),
+        "stream" (the same march, edges polled by the compute waves) or
+        "tiles" (block-Jacobi tile passes per step, tuned by set_options)."""
         _lib.check(self._L.burg_set_engine(self._h, _lib.ENGINES[engine], int(stream_w),
                                            int(tiles_target)))
         self.engine = dict(engine=engine, stream_w=stream_w, tiles_target=tiles_target)
 
     def set_problem(self, grid_x, grid_y, dt, mu, allow_nonsquare=False):
+        """Global grid arrays (a slab context picks its own rows)."""
         key = (np.asarray(grid_x).tobytes(), np.asarray(grid_y).tobytes(), float(dt),
                float(mu[0]), float(mu[1]), bool(allow_nonsquare))
         if key == self._problem:
             return
         ix, iy, src, lbc = fom_coefficients(grid_x, grid_y, dt, mu, allow_nonsquare)
-        if ix.size != self.nx or iy.size != self.ny:
+        if ix.size != self.nx or iy.size != self.ny_total:
             raise ValueError("grid does not match the context shape")
         _lib.check(self._L.burg_set_problem(self._h, _lib.dptr(ix), _lib.dptr(iy),
                                             _lib.dptr(src), _lib.dptr(lbc), float(dt)))
@@ -126,6 +146,15 @@ class FOMContext:
         w = np.empty(self.m)
         _lib.check(self._L.burg_download_state(self._h, _lib.dptr(w)))
         return w
+
+    def trajectory(self, num_steps, from_initial=True):
+        """num_steps steps in one launch from the uploaded initial state (or,
+        from_initial=False, from the resident state), every state kept in HBM;
+        returns stats (loop_ms = the launch's device time)."""
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_trajectory(self._h, int(num_steps), 1 if from_initial else 0,
+                                           ctypes.byref(st)))
+        return st.as_dict()
 
     def advance(self, num_steps, solver="march"):
         st = _lib.BurgStats()

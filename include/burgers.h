@@ -26,7 +26,7 @@
  *   - Every function returns BURG_OK (0) or a negative BURG_E* code; the
  *     message of the last failure on the calling thread is burg_last_error().
  *   - One context per host thread; a context owns its device buffers,
- *     its HIP stream and (multi-GPU) its RCCL communicator.
+ *     its HIP stream and (multi-GPU) its halo rings.
  */
 #ifndef BURGERS_H
 #define BURGERS_H
@@ -37,14 +37,14 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 2
+#define BURG_ABI_VERSION 3
 
 enum burg_status {
     BURG_OK = 0,
     BURG_EINVAL = -1,   /* bad argument (null pointer, size, option) */
     BURG_ESHAPE = -2,   /* grid shape not supported (e.g. nx != ny in strict mode) */
     BURG_EHIP = -3,     /* HIP runtime error */
-    BURG_ERCCL = -4,    /* RCCL error */
+    BURG_EHALO = -4,    /* multi-GPU halo ring (shared host memory) error */
     BURG_ENOMEM = -5,   /* device or pinned-host allocation failed */
     BURG_ENOCONV = -6,  /* solver hit its iteration cap (result still returned) */
     BURG_ENAN = -7,     /* non-finite residual or state */
@@ -80,11 +80,17 @@ typedef struct burg_stats {
     int64_t slow_diagonals;     /* streaming engine: diagonals that took the slow path */
     int64_t stream_launches;    /* streaming engine: launches (one per run chunk) */
     int64_t slow_ticks;         /* streaming engine: shader clocks spent on the slow path */
+    int64_t ieee_diagonals;     /* stream/pipe: diagonals redone with IEEE sqrt/div (range) */
+    int64_t comm_polls;         /* pipe engine: comm-wave polling rounds (all workgroups) */
 } burg_stats;
 
 enum burg_engine {
-    BURG_ENGINE_STREAM = 0,  /* one launch for many steps: exact pipelined march (default) */
-    BURG_ENGINE_TILES = 1    /* one step at a time: block-Jacobi tile passes (burg_set_options) */
+    BURG_ENGINE_STREAM = 0,  /* one launch for many steps: exact pipelined march, edges polled
+                                by the compute waves (any tile width) */
+    BURG_ENGINE_TILES = 1,   /* one step at a time: block-Jacobi tile passes (burg_set_options) */
+    BURG_ENGINE_PIPE = 2     /* default: the streaming march with LDS edges inside a workgroup
+                                and a comm wave per workgroup (tile width 8/16; falls back to
+                                STREAM on one GPU when the grid needs wider tiles) */
 };
 
 int burg_abi_version(void);
@@ -93,13 +99,18 @@ const char *burg_last_error(void);
 /* Create a context on HIP device `device` for an nx x ny grid (single GPU). */
 int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);
 
-/* Multi-GPU: this rank owns global rows [row0, row0 + nrows) of an
- * nx x ny_total grid.  `nccl_id` points to a 128-byte ncclUniqueId made by
- * rank 0 (burg_rccl_unique_id) and broadcast by the caller.  world == 1
- * behaves as burg_ctx_create. */
-int burg_rccl_unique_id(void *id_out_128_bytes);
+/* Multi-GPU (one process per GPU): this rank owns global rows
+ * [row0, row0 + nrows) of an nx x ny_total grid (rank 0 the bottom slab).
+ * The slabs exchange the one-way halo (north outflow of a slab's top row ->
+ * south inflow of the next slab) through rings in POSIX shared memory named
+ * from `halo_name` (the same job-unique string on every rank, 1-64 chars),
+ * which each GPU reads and writes directly while the time loop runs.  This
+ * call creates the ring this rank consumes; after EVERY rank has created its
+ * context (a host barrier), call burg_slab_connect to attach the ring this
+ * rank produces into.  world == 1 behaves as burg_ctx_create. */
 int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows,
-                         int rank, int world, const void *nccl_id, burg_ctx **out);
+                         int rank, int world, const char *halo_name, burg_ctx **out);
+int burg_slab_connect(burg_ctx *ctx);
 
 void burg_ctx_destroy(burg_ctx *ctx);
 
@@ -123,7 +134,7 @@ int burg_set_options(burg_ctx *ctx, int tile_w, int par_passes, double tol, int 
 
 /* March engine selection.  engine: BURG_ENGINE_*.  stream_w: streaming tile
  * width, a power of two in [8, 4096] (0: automatic, the narrowest width whose
- * tile count fits tiles_target).  tiles_target: wavefronts to aim for
+ * tile count fits tiles_target; the pipe engine takes 8 or 16).  tiles_target: wavefronts to aim for
  * (0: 1024 = one per SIMD of the MI355X).  The tile count is always capped by
  * what the device keeps resident at once (the engine needs every tile live). */
 int burg_set_engine(burg_ctx *ctx, int engine, int stream_w, int tiles_target);
@@ -155,6 +166,15 @@ int burg_run(burg_ctx *ctx, const double *w0, int num_steps, int solver,
 int burg_upload_state(burg_ctx *ctx, const double *w);
 int burg_advance(burg_ctx *ctx, int num_steps, int solver, burg_stats *stats);
 int burg_download_state(burg_ctx *ctx, double *w);
+
+/* One device-resident trajectory (the benchmark's unit of work): num_steps
+ * march steps in ONE launch from the last uploaded state (from_initial = 1,
+ * kept on the device by burg_upload_state) or from the resident state (0),
+ * every intermediate state kept in HBM (the snapshot matrix, in the engine's
+ * ring layout), the final state left resident.  Stream/pipe engines;
+ * stats->loop_ms is the launch's device time (HIP events on the context's
+ * stream). */
+int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *stats);
 
 #ifdef __cplusplus
 }

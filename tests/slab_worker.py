@@ -1,0 +1,32 @@
+"""One rank of tests/test_gpu_parity.py::test_slab_halo_two_processes_one_gpu
+(not a test module): its slab of an N x N grid, T steps from w0 = 1, on
+device 0, rendezvous over gloo; writes its slab snapshot matrix."""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    N, T, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    import torch.distributed as dist
+    from finitedifference_amd.dist import make_slab_context, slab_state
+    dist.init_process_group("gloo")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    ctx = make_slab_context(N, N, rank, world, device=0, dist=dist)
+    g = np.linspace(0, 100, N + 1)
+    ctx.set_problem(g, g, 0.05, (5.19, 0.026))
+    w0 = slab_state(np.ones(2 * N * N), N, N, rank, world)
+    dist.barrier()
+    snaps, st, _, _ = ctx.run(w0, T)
+    assert st["engine"] == 2
+    np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
+    dist.barrier()
+    ctx.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,6 +2,8 @@
 reference's golden vectors.  Bars: bitwise for equal op order and tiling,
 rel-L2 <= 1e-10 against the reference trajectory (north-star tolerance).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -262,3 +264,92 @@ def test_device_resident_advance_matches_run(gpu, engine):
     st = ctx.advance(T)
     assert st["steps"] == T
     assert np.array_equal(ctx.download(), full[:, T])
+
+
+# ----------------------------------------------------------- pipe engine --
+@pytest.mark.parametrize("N,ny,W,T", [
+    (13, 13, 8, 5), (64, 64, 16, 4), (100, 100, 0, 6), (250, 250, 0, 5), (130, 70, 8, 4),
+    (96, 200, 16, 4), (200, 129, 0, 7), (40, 64, 8, 9), (176, 64, 16, 3), (520, 300, 16, 3),
+    (1024, 1024, 0, 2)])
+def test_pipe_bitwise_sequential_march(gpu, orc, N, ny, W, T):
+    """The pipe engine IS the sequential march: every snapshot bit-equal to
+    the oracle's orc_march_step trajectory, for any tiling: one tile, partial
+    strips, partial workgroups (tile columns not a multiple of 4), non-square."""
+    P = orc.Problem(N, ny, Ly=100.0 * ny / N, allow_nonsquare=(N != ny))
+    w0 = state_after(orc, P, 3)
+    ctx = FOMContext_for(N, ny, engine="pipe", stream_w=W)
+    ctx.set_problem(P.grid_x, P.grid_y, P.dt, P.mu, allow_nonsquare=(N != ny))
+    snaps, st, its, _ = ctx.run(w0, T)
+    ref, _, _ = P.fom(w0, T)
+    assert st["engine"] == 2, "pipe engine expected (no fallback at these sizes)"
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+    assert st["steps"] == T and st["stream_launches"] == 1
+    assert st["tile_marches"] == T * st["stream_tiles"]
+
+
+def test_pipe_many_launches_cycle_sentinel_colours(gpu, orc):
+    """Launch lengths that are not multiples of the mailbox depth (8 steps):
+    the absolute step counter carries the sentinel colours across launches."""
+    N = 136
+    P = orc.Problem(N)
+    ks = (1, 2, 3, 5, 7, 9, 11, 13)
+    ref, _, _ = P.fom(np.ones(P.m), sum(ks))
+    ctx = make_ctx(N, engine="pipe", stream_w=8)
+    ctx.upload(np.ones(P.m))
+    for k in ks:
+        st = ctx.advance(k)
+        assert st["engine"] == 2
+    assert np.array_equal(ctx.download(), ref[sum(ks)])
+
+
+def test_pipe_and_stream_engines_agree(gpu):
+    N, T = 300, 6
+    a = make_ctx(N, engine="pipe").run(np.ones(2 * N * N), T)[0]
+    b = make_ctx(N, engine="stream").run(np.ones(2 * N * N), T)[0]
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.parametrize("N,world,T", [(128, 2, 9), (150, 3, 7)])
+def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T):
+    """Multi-GPU path, rehearsed on one GPU: `world` processes, one slab each,
+    all on device 0, exchanging the halo through the shared host rings while
+    their time loops run concurrently.  The assembled trajectory is the
+    single-grid sequential march bit for bit."""
+    import subprocess
+    import sys
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    worker = os.path.join(os.path.dirname(__file__), "slab_worker.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20")
+        procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path)],
+                                      env=env))
+    codes = [p.wait(timeout=110) for p in procs]
+    assert codes == [0] * world, codes
+    from finitedifference_amd.dist import assemble_snaps
+    parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
+    snaps = assemble_snaps(parts, N, N)
+    ref, _, _ = orc.Problem(N).fom(np.ones(2 * N * N), T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+
+
+def test_trajectory_from_initial_is_repeatable(gpu, orc):
+    """burg_trajectory (the bench's unit of work): from the uploaded w0 every
+    time, or continuing from the resident state; final states = oracle."""
+    N, T = 144, 11
+    P = orc.Problem(N)
+    ref, _, _ = P.fom(np.ones(P.m), 2 * T)
+    ctx = make_ctx(N)
+    ctx.upload(np.ones(P.m))
+    for _ in range(2):
+        st = ctx.trajectory(T)
+        assert st["engine"] == 2 and st["steps"] == T
+        assert np.array_equal(ctx.download(), ref[T])
+    ctx.trajectory(T, from_initial=False)
+    assert np.array_equal(ctx.download(), ref[2 * T])
