@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--stream-w", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stencil-nx", type=int, default=8192,
+                    help="grid of the residual / J.x roofline probe (0: skip)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -89,6 +91,30 @@ def cpu_baseline(nx, seconds):
             "sample": f"oracle Newton (reference algorithm, exact block solve in place of "
                       f"SuperLU) on {nx}x{nx}, first {steps} of the 500 steps from w0=1, "
                       f"{dt:.1f} s, 1 thread"}
+
+
+def stencil_roofline(nx, reps=20, pmc_file=None):
+    """Residual (K1) and Jacobian action (K2) -- the HBM-bound stencils of the
+    reference's Newton path (C/hypernet2D.py:2512-2570, 2627-2656) -- on an
+    nx x nx grid (north star: >= 40 % of HBM roofline at 8192^2).  Algorithmic
+    bytes per launch: 48 B per cell; mean launch time
+    from HIP events on the library's stream."""
+    from finitedifference_amd.solver import FOMContext
+    ctx = FOMContext(nx, nx, engine="pipe")
+    g = np.linspace(0, 100, nx + 1)
+    ctx.set_problem(g, g, DT, MU)
+    rng = np.random.default_rng(1234557)
+    ctx.upload(rng.uniform(1.0, 6.0, ctx.m))
+    out = {"grid": f"{nx}x{nx}", "alg_bytes_per_cell": 48, "peak": HBM_PEAK_GBS, "unit": "GB/s"}
+    for k in ("residual", "jvp"):
+        ms = ctx.kernel_bench(k, reps)
+        gbs = 48.0 * nx * nx / (ms * 1e-3) / 1e9
+        traffic, tsrc = read_pmc(pmc_file, f"stencil_{k}:{nx}x{nx}") if pmc_file else (None, None)
+        out[k] = {"avg_launch_ms": round(ms, 5), "achieved": round(gbs, 1),
+                  "frac": round(gbs / HBM_PEAK_GBS, 4), "alg_bytes": 48 * nx * nx,
+                  "traffic": traffic, "traffic_source": tsrc}
+    ctx.close()
+    return out
 
 
 def read_pmc(path, key):
@@ -198,6 +224,8 @@ def main():
                 "traffic_source": tsrc,
             },
         }
+        if world == 1 and args.stencil_nx > 0:
+            out["stencil_roofline"] = stencil_roofline(args.stencil_nx, pmc_file=args.pmc_file)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nx, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -26,7 +26,9 @@ EXPORTS = (
     "burg_slab_connect", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
+    "burg_kernel_bench",
 )
+KERNELS = {"residual": 0, "jvp": 1}
 
 
 class BurgStats(ctypes.Structure):
@@ -116,6 +118,7 @@ def load(path=None):
             "burg_trajectory": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(BurgStats)]),
             "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+            "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -1066,6 +1066,37 @@ int burg_download_state(burg_ctx *c, double *w)
     return BURG_OK;
 }
 
+int burg_kernel_bench(burg_ctx *c, int which, int reps, double *avg_ms)
+{
+    if (int e = check_ready(c)) return e;
+    if (!avg_ms) return fail(BURG_EINVAL, "null avg_ms");
+    if (reps < 1) return fail(BURG_EINVAL, "reps < 1");
+    if (which != BURG_KERNEL_RESIDUAL && which != BURG_KERNEL_JVP)
+        return fail(BURG_EINVAL, "unknown kernel %d", which);
+    if (c->world > 1) return fail(BURG_EINVAL, "burg_kernel_bench: single-GPU contexts only");
+    if (!c->d_w0) return fail(BURG_ESTATE, "burg_kernel_bench: call burg_upload_state first");
+    if (int e = ensure_scratch(c)) return e;
+    const size_t bytes = c->m() * sizeof(double);
+    HIPCHK(hipMemcpyAsync(c->d_x, c->d_w0, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_d, c->d_state[c->cur], bytes, hipMemcpyDeviceToDevice,
+                          c->stream));
+    auto once = [&]() -> int {
+        if (which == BURG_KERNEL_RESIDUAL)
+            return launch_residual(c->cf, c->d_x, c->d_d, c->d_r, c->d_partials, c->d_sumsq,
+                                   nullptr, nullptr, c->stream);
+        return launch_jvp(c->cf, c->d_x, c->d_d, c->d_r, c->stream);
+    };
+    CHK(once());  // warm (code object, TLB)
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    for (int i = 0; i < reps; ++i) CHK(once());
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    HIPCHK(hipEventSynchronize(c->ev1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+    *avg_ms = (double)ms / reps;
+    return BURG_OK;
+}
+
 int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
 {
     if (int e = check_ready(c)) return e;

@@ -14,8 +14,28 @@ namespace {
 
 constexpr int kBlock = 256;
 
-// Sum of squares of the two planes' cells this block owns, tree-reduced in
-// a fixed order (deterministic).
+// Row-marching layout of the two stencils (K1, K2): a workgroup owns a strip
+// of 256 columns x `rows` rows and walks it bottom to top.  Every cell's
+// u, v (and up, vp or xu, xv) are loaded from HBM exactly once: the south
+// neighbour's terms are the previous row's, carried in registers, and the
+// west neighbour's terms are the left lane's, moved by one DPP wave shift
+// (lane 0 of each wave computes its west terms from its own loads).  The
+// neighbour terms are the SAME expressions the neighbour evaluates for
+// itself, so the result is bitwise the one-cell-per-thread formulation
+// (op order of oracle/burgers_oracle.c, -ffp-contract=off).
+
+// lane i <- lane i-1 (wave shift); lane 0 keeps `old0`
+__device__ __forceinline__ double wave_shr1(double old0, double x)
+{
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old0), __double2loint(x), 0x138,
+                                               0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old0), __double2hiint(x), 0x138,
+                                               0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Sum of squares of the cells this block owns, tree-reduced in a fixed
+// order (deterministic).
 __device__ __forceinline__ void block_sumsq(double x, double *partials)
 {
     __shared__ double red[kBlock];
@@ -25,64 +45,105 @@ __device__ __forceinline__ void block_sumsq(double x, double *partials)
         if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partials[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+}
+
+// rows per workgroup: enough workgroups to fill the chip (>= 2048), at
+// most 64 rows (carry reuse saturates long before)
+__host__ __device__ inline int stencil_rows(int nx, int ny)
+{
+    const int nbx = (nx + kBlock - 1) / kBlock;
+    int rows = 64;
+    while (rows > 4 && (long long)nbx * ((ny + rows - 1) / rows) < 2048) rows >>= 1;
+    return rows;
 }
 
 // halo_w / halo_wp: [u row | v row] of the row below this slab (nullptr =
 // domain boundary).
-__global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const double *w,
-                                                          const double *wp, double *res,
-                                                          double *partials,
-                                                          const double *halo_w,
-                                                          const double *halo_wp)
+__global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const double *__restrict__ w,
+                                                          const double *__restrict__ wp,
+                                                          double *__restrict__ res,
+                                                          double *__restrict__ partials,
+                                                          const double *__restrict__ halo_w,
+                                                          const double *__restrict__ halo_wp,
+                                                          int rows)
 {
     const int nx = cf.nx, ny = cf.ny;
     const size_t n = (size_t)nx * ny;
-    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    double sq = 0.0;
-    if (i < n) {
-        const int r = (int)(i / nx), c = (int)(i - (size_t)r * nx);
-        const double a = cf.alpha;
-        const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
-        const double ay = a * cf.inv_dy[r];
-        const double ax = a * cf.inv_dx[c];
-        const double Su = 0.5 * (u[i] * u[i]) + 0.5 * (up[i] * up[i]);
-        const double Sv = 0.5 * (v[i] * v[i]) + 0.5 * (vp[i] * vp[i]);
-        const double Suv = (0.5 * u[i]) * v[i] + (0.5 * up[i]) * vp[i];
-        double dxu = ax * Su, dyuv = ay * Suv, dyv = ay * Sv, dxuv = cf.inv_dx[c] * Suv;
-        if (c > 0) {
-            const size_t j = i - 1;
-            const double axw = a * cf.inv_dx[c - 1];
-            const double SuW = 0.5 * (u[j] * u[j]) + 0.5 * (up[j] * up[j]);
-            const double SuvW = (0.5 * u[j]) * v[j] + (0.5 * up[j]) * vp[j];
-            dxu = dxu + (-axw) * SuW;
-            dxuv = dxuv + (-cf.inv_dx[c - 1]) * SuvW;
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    const int r0 = blockIdx.y * rows;
+    const int r1 = min(ny, r0 + rows);
+    const bool colok = c < nx;
+    const int cc = colok ? c : nx - 1;  // padding lanes mirror a real column, store nothing
+    const bool lane0 = (threadIdx.x & (kWave - 1)) == 0;
+    const bool west = c > 0;
+    const double a = cf.alpha;
+    const double idx = cf.inv_dx[cc];
+    const double ax = a * idx;
+    const double idxw = west ? cf.inv_dx[cc - 1] : 0.0;
+    const double axw = a * idxw;
+    const double srcc = cf.src[cc];
+    const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
+
+    // south carry: Sv, Suv of the row below r0 and a*inv_dy of that row
+    bool has_s = false;
+    double SvS = 0.0, SuvS = 0.0, ays = 0.0;
+    if (r0 > 0 || halo_w != nullptr) {
+        double uS, vS, upS, vpS;
+        if (r0 > 0) {
+            const size_t j = (size_t)(r0 - 1) * nx + cc;
+            uS = u[j], vS = v[j], upS = up[j], vpS = vp[j];
+        } else {
+            uS = halo_w[cc], vS = halo_w[nx + cc], upS = halo_wp[cc], vpS = halo_wp[nx + cc];
         }
-        if (r > 0 || halo_w != nullptr) {
-            double uS, vS, upS, vpS;
-            if (r > 0) {
-                const size_t j = i - (size_t)nx;
-                uS = u[j], vS = v[j], upS = up[j], vpS = vp[j];
-            } else {
-                uS = halo_w[c], vS = halo_w[nx + c], upS = halo_wp[c], vpS = halo_wp[nx + c];
-            }
-            const double ays = a * cf.inv_dy[r - 1];
-            const double SvS = 0.5 * (vS * vS) + 0.5 * (vpS * vpS);
-            const double SuvS = (0.5 * uS) * vS + (0.5 * upS) * vpS;
+        ays = a * cf.inv_dy[r0 - 1];
+        SvS = 0.5 * (vS * vS) + 0.5 * (vpS * vpS);
+        SuvS = (0.5 * uS) * vS + (0.5 * upS) * vpS;
+        has_s = true;
+    }
+    double sq = 0.0;
+    for (int r = r0; r < r1; ++r) {
+        const size_t i = (size_t)r * nx + cc;
+        const double ui = u[i], vi = v[i], upi = up[i], vpi = vp[i];
+        double SuW0 = 0.0, SuvW0 = 0.0;
+        if (lane0 && west) {
+            const size_t j = i - 1;
+            const double uj = u[j], vj = v[j], upj = up[j], vpj = vp[j];
+            SuW0 = 0.5 * (uj * uj) + 0.5 * (upj * upj);
+            SuvW0 = (0.5 * uj) * vj + (0.5 * upj) * vpj;
+        }
+        const double ay = a * cf.inv_dy[r];
+        const double Su = 0.5 * (ui * ui) + 0.5 * (upi * upi);
+        const double Sv = 0.5 * (vi * vi) + 0.5 * (vpi * vpi);
+        const double Suv = (0.5 * ui) * vi + (0.5 * upi) * vpi;
+        const double SuW = wave_shr1(SuW0, Su);
+        const double SuvW = wave_shr1(SuvW0, Suv);
+        double dxu = ax * Su, dyuv = ay * Suv, dyv = ay * Sv, dxuv = idx * Suv;
+        if (west) {
+            dxu = dxu + (-axw) * SuW;
+            dxuv = dxuv + (-idxw) * SuvW;
+        }
+        if (has_s) {
             dyuv = dyuv + (-ays) * SuvS;
             dyv = dyv + (-ays) * SvS;
         }
-        double ru = u[i] - up[i];
+        double ru = ui - upi;
         ru = ru + dxu;
         ru = ru + dyuv;
-        ru = ru - cf.src[c];
+        ru = ru - srcc;
         ru = ru - (c == 0 ? cf.lbc[r] : 0.0);
-        double rv = v[i] - vp[i];
+        double rv = vi - vpi;
         rv = rv + dyv;
         rv = rv + a * dxuv;
-        res[i] = ru;
-        res[n + i] = rv;
-        sq = ru * ru + rv * rv;
+        if (colok) {
+            __builtin_nontemporal_store(ru, &res[i]);
+            __builtin_nontemporal_store(rv, &res[n + i]);
+            sq += ru * ru + rv * rv;
+        }
+        SvS = Sv;
+        SuvS = Suv;
+        ays = ay;
+        has_s = true;
     }
     block_sumsq(sq, partials);
 }
@@ -102,36 +163,73 @@ __global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double *part
     if (threadIdx.x == 0) *out = red[0];
 }
 
-__global__ __launch_bounds__(kBlock) void jvp_kernel(Coeffs cf, const double *w,
-                                                     const double *x, double *y)
+// J(w) x: per cell the terms t1 = (ax u) xu, t2 = (0.5 ay) m, t3 = (ay v) xv,
+// t4 = (0.5 ax) m with m = v xu + u xv; the west cell's t1, t4 and the
+// south cell's t2, t3 enter with a minus sign (exact_jac2D, :2627-2656).
+__global__ __launch_bounds__(kBlock) void jvp_kernel(Coeffs cf, const double *__restrict__ w,
+                                                     const double *__restrict__ x,
+                                                     double *__restrict__ y, int rows)
 {
     const int nx = cf.nx, ny = cf.ny;
     const size_t n = (size_t)nx * ny;
-    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const int r = (int)(i / nx), c = (int)(i - (size_t)r * nx);
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    const int r0 = blockIdx.y * rows;
+    const int r1 = min(ny, r0 + rows);
+    const bool colok = c < nx;
+    const int cc = colok ? c : nx - 1;
+    const bool lane0 = (threadIdx.x & (kWave - 1)) == 0;
+    const bool west = c > 0;
     const double a = cf.alpha;
+    const double ax = a * cf.inv_dx[cc];
+    const double axw = west ? a * cf.inv_dx[cc - 1] : 0.0;
     const double *u = w, *v = w + n, *xu = x, *xv = x + n;
-    const double ax = a * cf.inv_dx[c], ay = a * cf.inv_dy[r];
-    const double m = v[i] * xu[i] + u[i] * xv[i];
-    double yu = xu[i] + ax * u[i] * xu[i] + 0.5 * ay * m;
-    double yv = xv[i] + ay * v[i] * xv[i] + 0.5 * ax * m;
-    if (c > 0) {
-        const size_t j = i - 1;
-        const double axw = a * cf.inv_dx[c - 1];
-        const double mW = v[j] * xu[j] + u[j] * xv[j];
-        yu -= axw * u[j] * xu[j];
-        yv -= 0.5 * axw * mW;
-    }
-    if (r > 0) {
-        const size_t j = i - (size_t)nx;
-        const double ays = a * cf.inv_dy[r - 1];
+
+    bool has_s = false;
+    double t2S = 0.0, t3S = 0.0;
+    if (r0 > 0) {
+        const size_t j = (size_t)(r0 - 1) * nx + cc;
+        const double ays = a * cf.inv_dy[r0 - 1];
         const double mS = v[j] * xu[j] + u[j] * xv[j];
-        yu -= 0.5 * ays * mS;
-        yv -= ays * v[j] * xv[j];
+        t2S = 0.5 * ays * mS;
+        t3S = ays * v[j] * xv[j];
+        has_s = true;
     }
-    y[i] = yu;
-    y[n + i] = yv;
+    for (int r = r0; r < r1; ++r) {
+        const size_t i = (size_t)r * nx + cc;
+        const double ui = u[i], vi = v[i], xui = xu[i], xvi = xv[i];
+        double t1W0 = 0.0, t4W0 = 0.0;
+        if (lane0 && west) {
+            const size_t j = i - 1;
+            const double mW = v[j] * xu[j] + u[j] * xv[j];
+            t1W0 = axw * u[j] * xu[j];
+            t4W0 = 0.5 * axw * mW;
+        }
+        const double ay = a * cf.inv_dy[r];
+        const double m = vi * xui + ui * xvi;
+        const double t1 = ax * ui * xui;
+        const double t2 = 0.5 * ay * m;
+        const double t3 = ay * vi * xvi;
+        const double t4 = 0.5 * ax * m;
+        const double t1W = wave_shr1(t1W0, t1);
+        const double t4W = wave_shr1(t4W0, t4);
+        double yu = xui + t1 + t2;
+        double yv = xvi + t3 + t4;
+        if (west) {
+            yu -= t1W;
+            yv -= t4W;
+        }
+        if (has_s) {
+            yu -= t2S;
+            yv -= t3S;
+        }
+        if (colok) {
+            __builtin_nontemporal_store(yu, &y[i]);
+            __builtin_nontemporal_store(yv, &y[n + i]);
+        }
+        t2S = t2;
+        t3S = t3;
+        has_s = true;
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void axpy_neg_kernel(double *w, const double *d, size_t m)
@@ -168,8 +266,8 @@ __global__ __launch_bounds__(256) void transpose_kernel(StatePtrs sp, int nstate
 
 int residual_partials_count(const Coeffs &cf)
 {
-    const size_t n = (size_t)cf.nx * cf.ny;
-    return (int)((n + kBlock - 1) / kBlock);
+    const int rows = stencil_rows(cf.nx, cf.ny);
+    return ((cf.nx + kBlock - 1) / kBlock) * ((cf.ny + rows - 1) / rows);
 }
 
 int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
@@ -177,15 +275,18 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
                     const double *halo_wp, hipStream_t st)
 {
     const int nb = residual_partials_count(cf);
-    residual_kernel<<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp);
+    const int rows = stencil_rows(cf.nx, cf.ny);
+    const dim3 grid((cf.nx + kBlock - 1) / kBlock, (cf.ny + rows - 1) / rows);
+    residual_kernel<<<grid, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows);
     if (sumsq) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y, hipStream_t st)
 {
-    const size_t n = (size_t)cf.nx * cf.ny;
-    jvp_kernel<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(cf, w, x, y);
+    const int rows = stencil_rows(cf.nx, cf.ny);
+    const dim3 grid((cf.nx + kBlock - 1) / kBlock, (cf.ny + rows - 1) / rows);
+    jvp_kernel<<<grid, kBlock, 0, st>>>(cf, w, x, y, rows);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -156,6 +156,14 @@ class FOMContext:
                                            ctypes.byref(st)))
         return st.as_dict()
 
+    def kernel_bench(self, kernel="residual", reps=20):
+        """Mean device time (ms) of one launch of the residual or J.x stencil
+        on device-resident operands (burg_kernel_bench; upload() first)."""
+        ms = ctypes.c_double(0.0)
+        _lib.check(self._L.burg_kernel_bench(self._h, _lib.KERNELS[kernel], int(reps),
+                                             ctypes.byref(ms)))
+        return ms.value
+
     def advance(self, num_steps, solver="march"):
         st = _lib.BurgStats()
         _lib.check(self._L.burg_advance(self._h, int(num_steps), _lib.SOLVERS[solver],

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 3
+#define BURG_ABI_VERSION 4
 
 enum burg_status {
     BURG_OK = 0,
@@ -54,6 +54,11 @@ enum burg_status {
 enum burg_solver {
     BURG_SOLVER_MARCH = 0,  /* closed-form upwind march (default, exact implicit step) */
     BURG_SOLVER_NEWTON = 1  /* newton_raphson + exact block solve (reference algorithm) */
+};
+
+enum burg_kernel {
+    BURG_KERNEL_RESIDUAL = 0,  /* residual stencil + its norm reduction (burg_residual) */
+    BURG_KERNEL_JVP = 1        /* Jacobian action J(w) x (burg_jvp) */
 };
 
 typedef struct burg_ctx burg_ctx;
@@ -166,6 +171,15 @@ int burg_run(burg_ctx *ctx, const double *w0, int num_steps, int solver,
 int burg_upload_state(burg_ctx *ctx, const double *w);
 int burg_advance(burg_ctx *ctx, int num_steps, int solver, burg_stats *stats);
 int burg_download_state(burg_ctx *ctx, double *w);
+
+/* Roofline probe of the HBM-bound stencils: runs
+ * kernel `which` (burg_kernel) `reps` times on device-resident operands (the
+ * last uploaded state as w, the resident state as wp / x; results discarded)
+ * and returns the mean device time per launch (HIP events on the context's
+ * stream).  Algorithmic bytes per launch: 48 B per cell (read u, v and
+ * up, vp / xu, xv; write two planes).  Single-GPU contexts; call
+ * burg_upload_state first. */
+int burg_kernel_bench(burg_ctx *ctx, int which, int reps, double *avg_ms);
 
 /* One device-resident trajectory (the benchmark's unit of work): num_steps
  * march steps in ONE launch from the last uploaded state (from_initial = 1,

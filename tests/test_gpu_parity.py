@@ -68,6 +68,33 @@ def test_jvp_bitwise_vs_oracle_and_reference(gpu, orc, N):
         assert np.allclose(y[g["n250_res_idx"]], g["n250_jx_at"], rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("nx,ny", [(300, 70), (520, 300), (257, 33), (1024, 1024)])
+def test_stencils_bitwise_ragged_strips(gpu, orc, nx, ny):
+    """Row-marching stencils (256-column strips, south terms carried, west
+    terms by DPP): ragged last strip, several strips, partial row blocks --
+    bit-equal to the oracle's one-cell-at-a-time restatement."""
+    P = orc.Problem(nx, ny, Ly=100.0 * ny / nx, allow_nonsquare=(nx != ny))
+    rng = np.random.default_rng(1234557)
+    w = rng.uniform(1.0, 6.0, P.m)
+    wp = rng.uniform(1.0, 6.0, P.m)
+    x = rng.standard_normal(P.m)
+    ctx = make_ctx(nx, ny=ny)
+    ctx.set_problem(P.grid_x, P.grid_y, P.dt, P.mu, allow_nonsquare=(nx != ny))
+    r, nrm = ctx.residual(w, wp)
+    ro = P.residual(w, wp)
+    assert np.array_equal(r, ro)
+    assert abs(nrm - np.linalg.norm(ro)) <= 1e-13 * np.linalg.norm(ro)
+    assert np.array_equal(ctx.jvp(w, x), P.jvp(w, x))
+
+
+def test_kernel_bench_runs(gpu):
+    ctx = make_ctx(512)
+    ctx.upload(np.ones(ctx.m))
+    for k in ("residual", "jvp"):
+        ms = ctx.kernel_bench(k, reps=3)
+        assert 0.0 < ms < 100.0
+
+
 @pytest.mark.parametrize("N", [16, 64])
 def test_block_solve_matches_spsolve(gpu, orc, N):
     g = golden("ref_ops.npz")
