@@ -4,20 +4,22 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--time-steps T]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Unit of work ("step"): ONE FOM trajectory, i.e. one pass of the hot path =
-the reference's run_fom.main time loop (C/run_fom.py:24-43 ->
-inviscid_burgers_implicit2D, C/hypernet2D.py:72-131): T = 500 implicit time
-steps (dt = 0.05, mu = (5.19, 0.026)) of the whole grid, every intermediate
-state kept resident in HBM (the snapshot matrix, engine ring layout), solved
-exactly by the HIP march in one launch.  Every bench step runs the same
-trajectory from w0 = 1 (kept on the device since the one upload).
+Unit of work ("step"): ONE SNAPSHOT SWEEP = the reference's FOM snapshot
+generation for the ROM training set (C/run_prom.py:59-71 ->
+load_or_compute_snaps for each of the 9 get_snapshot_params mu,
+C/train_autoencoder.py:63-72; each one run_fom.main's time loop,
+inviscid_burgers_implicit2D, C/hypernet2D.py:72-131): 9 trajectories of
+T = 500 implicit time steps (dt = 0.05, w0 = 1) of the whole grid, every
+intermediate state kept resident in HBM (the 9 snapshot matrices, engine ring
+layout), solved exactly by the HIP march in ONE pipelined launch
+(burg_sweep).  --sweep 1 times single trajectories at mu = (5.19, 0.026)
+(burg_trajectory) instead.
 
 Workload (BASELINE.json configs[1]): 1024 x 1024 cells per GPU, fp64.  N > 1:
 weak scaling by row slabs, rank k owning rows [1024k, 1024k+1024) of a
 1024 x 1024N grid (same cell size), the one-way halo streamed GPU-to-GPU
-during the launch.  value = N * 1024^2 * T * K / (max
-over ranks of the wall time of the K timed trajectories), inputs resident in
-HBM.
+during the launch.  value = N * 1024^2 * T * 9 * K / (max
+over ranks of the wall time of the K timed sweeps), inputs resident in HBM.
 
 Extra JSON objects: roofline (the march kernel: algorithmic 32 B per
 cell-update = read the previous state u, v + write the new state u, v,
@@ -48,8 +50,11 @@ METRIC = "Mcell-updates/s (fp64) for 2D Burgers FOM; % HBM roofline at 1/2/4/8 G
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed trajectories")
-    ap.add_argument("--warmup", type=int, default=3, help="untimed trajectories")
+    ap.add_argument("--steps", type=int, default=10, help="timed sweeps")
+    ap.add_argument("--warmup", type=int, default=2, help="untimed sweeps")
+    ap.add_argument("--sweep", type=int, default=9,
+                    help="trajectories per step: the first N of the 9 training mu "
+                         "(get_snapshot_params); 1 = one trajectory at mu=(5.19, 0.026)")
     ap.add_argument("--time-steps", type=int, default=500,
                     help="implicit steps per trajectory (run_fom.py: 500)")
     ap.add_argument("--nx", type=int, default=1024)
@@ -155,6 +160,14 @@ def main():
     gy = np.linspace(0, 100.0 * ny / nx, ny + 1)  # same cell size: weak scaling
     ctx.set_problem(gx, gy, DT, MU, allow_nonsquare=(nx != ny))
     ctx.upload(np.ones(ctx.m))
+    from finitedifference_amd.config import get_snapshot_params
+    mus = get_snapshot_params()[:args.sweep] if args.sweep > 1 else [MU]
+    nmu = len(mus)
+
+    def one_step():
+        if nmu == 1:
+            return ctx.trajectory(T)
+        return ctx.sweep(mus, T, keep_snaps=False)[1]
 
     def barrier():
         if world > 1:
@@ -163,14 +176,16 @@ def main():
 
     for _ in range(args.warmup):
         barrier()
-        ctx.trajectory(T)
+        one_step()
     barrier()
     t0 = time.perf_counter()
     kern_ms = 0.0
+    launches = 0
     st = None
     for _ in range(args.steps):
-        st = ctx.trajectory(T)
+        st = one_step()
         kern_ms += st["loop_ms"]
+        launches += max(1, st["stream_launches"])
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -178,16 +193,18 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     cells = nx * ny  # whole job
-    value = cells * T * args.steps / elapsed / 1e6
+    value = cells * T * nmu * args.steps / elapsed / 1e6
 
     if rank == 0:
         eng = {0: "stream", 2: "pipe"}.get(st["engine"], str(st["engine"]))
-        kname = f"pipe_kernel<{st['stream_w']}>" if st["engine"] == 2 else \
-            f"stream_kernel<{st['stream_w']}>"
-        per_launch = BYTES_PER_CELL_UPDATE * nx * rows * T  # this rank's kernel
-        avg_ms = kern_ms / max(1, args.steps)
+        kname = (f"pipe_kernel<{st['stream_w']}, {'true' if nmu > 1 else 'false'}>"
+                 if st["engine"] == 2 else f"stream_kernel<{st['stream_w']}>")
+        # this rank's kernel: all launches of the timed region
+        per_launch = BYTES_PER_CELL_UPDATE * nx * rows * T * nmu * args.steps / launches
+        avg_ms = kern_ms / launches
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = read_pmc(args.pmc_file, f"{eng}:{nx}x{rows}:T{T}")
+        key = f"{eng}:{nx}x{rows}:T{T}" + (f"x{nmu}" if nmu > 1 else "")
+        traffic, tsrc = read_pmc(args.pmc_file, key)
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -200,13 +217,19 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic: reference initial state w0=1, mu=(5.19,0.026), dt=0.05; "
-                    "each step = one 500-step FOM trajectory from w0 (run_fom.main's loop)",
+            "data": ("synthetic: reference initial state w0=1, dt=0.05; each step = the FOM "
+                     f"snapshot sweep over the first {nmu} training mu of get_snapshot_params "
+                     f"(C/train_autoencoder.py:63-72, as run_prom.py:59-71), {T} steps each"
+                     if nmu > 1 else
+                     "synthetic: reference initial state w0=1, mu=(5.19,0.026), dt=0.05; "
+                     "each step = one 500-step FOM trajectory from w0 (run_fom.main's loop)"),
             "config": {
                 "workload": f"implicit 2D inviscid Burgers FOM (run_fom time loop), "
                             f"{nx}x{rows} cells per GPU (grid {nx}x{ny}), fp64, "
-                            f"{T} implicit steps per trajectory, exact march on MI355X",
+                            f"{T} implicit steps per trajectory, {nmu} trajectories (mu) "
+                            f"per step, exact march on MI355X",
                 "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T,
+                "trajectories_per_step": nmu,
                 "parallelism": f"row-slab x{world}",
             },
             "engine": {"name": eng, "tile_w": st["stream_w"], "tiles": st["stream_tiles"],
@@ -220,7 +243,7 @@ def main():
                 "kernel": kname,
                 "per_launch_alg_bytes": int(per_launch),
                 "avg_launch_ms": round(avg_ms, 5),
-                "launches": args.steps,
+                "launches": launches,
                 "traffic_source": tsrc,
             },
         }

@@ -18,3 +18,11 @@ GRID_X, GRID_Y = make_2D_grid(XL, XU, XL, XU, NUM_CELLS, NUM_CELLS)
 MU1_RANGE = 4.25, 5.5
 MU2_RANGE = 0.015, 0.03
 SAMPLES_PER_MU = 3
+
+
+def get_snapshot_params():
+    """The 9 training parameters (C/train_autoencoder.py:63-72): mu1 outer,
+    mu2 inner, linspace over MU1_RANGE x MU2_RANGE with SAMPLES_PER_MU each."""
+    mu1 = np.linspace(MU1_RANGE[0], MU1_RANGE[1], SAMPLES_PER_MU)
+    mu2 = np.linspace(MU2_RANGE[0], MU2_RANGE[1], SAMPLES_PER_MU)
+    return [[a, b] for a in mu1 for b in mu2]

@@ -106,6 +106,7 @@ struct StreamArgs {
 // use two sentinel colours so that a slot's emptiness is tied to a step.
 constexpr int kPipeR = 8;   // global mailbox slots (steps) per edge, power of two
 constexpr int kPipeRL = 4;  // LDS ring slots (steps) per intra-workgroup edge
+constexpr int kPipeSweepMax = 10;  // trajectories per sweep launch (LDS-resident tables)
 
 struct PipeArgs {
     Coeffs cf;
@@ -122,6 +123,13 @@ struct PipeArgs {
     size_t halo_bytes;
     long long origin, L;  // ring entry of diagonal 0, ring length
     int K;                // steps of this launch
+    // Parameter sweep (burg_sweep): the launch runs K / T trajectories of T
+    // steps back to back, each from the initial state, trajectory j with
+    // its own source / inlet coefficients.  T == K, colc_b == nullptr: one
+    // trajectory (colc, cf.lbc).
+    int T;
+    const d2 *colc_b;     // [K/T][ntj*W] {hx, src_j}
+    const double *lbc_b;  // [K/T][ny] inlet term of trajectory j, this slab's rows
     int qbase;            // absolute step of local step 0, mod 2*kPipeR (sentinel colour)
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
@@ -153,12 +161,14 @@ bool stream_width_supported(int W);
 int stream_max_resident_blocks(int W, int *per_cu, int *cus);
 int launch_stream(const StreamArgs &a, int W, hipStream_t st);
 int launch_colc(const Coeffs &cf, int ncols_pad, void *colc, hipStream_t st);
+int launch_colc_batch(const Coeffs &cf, int nb, const double *src_b, int ncols_pad, void *colc_b,
+                      hipStream_t st);
 int launch_fill_sentinel(void *p, size_t n16, hipStream_t st);
 int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st);
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
                         int ldo, hipStream_t st);
 bool pipe_width_supported(int W);
-int pipe_max_resident_blocks(int W);
+int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,

@@ -120,6 +120,11 @@ struct burg_ctx {
     // strip, absolute step counter mod 2*kPipeR (mailbox sentinel colour)
     int eng_eff = BURG_ENGINE_STREAM;
     int nwj = 0, qbase = 0;
+    // parameter sweep of the next pipe launch (burg_sweep): steps per
+    // trajectory and the per-trajectory coefficient tables (0/nullptr: none)
+    int sw_T = 0;
+    const d2 *sw_colc = nullptr;
+    const double *sw_lbc = nullptr;
     long long spin_ticks = 500000000LL;  // 5 s of s_memrealtime (100 MHz)
     // multi-GPU halo rings (pinned shared host memory)
     std::string halo_name;
@@ -460,6 +465,9 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.origin = origin;
     a.L = L;
     a.K = K;
+    a.T = c->sw_T > 0 ? c->sw_T : K;
+    a.colc_b = c->sw_T > 0 ? c->sw_colc : nullptr;
+    a.lbc_b = c->sw_T > 0 ? c->sw_lbc : nullptr;
     a.qbase = c->qbase;
     a.nti = c->sp.nti;
     a.ntj = c->sp.ntj;
@@ -1149,6 +1157,176 @@ int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st
     if (c->engine == BURG_ENGINE_TILES)
         return fail(BURG_EINVAL, "burg_trajectory runs on the stream/pipe engines");
     return stream_trajectory(c, num_steps, from_initial != 0, st);
+}
+
+int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,
+               double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (st) std::memset(st, 0, sizeof *st);
+    if (nmu < 1) return fail(BURG_EINVAL, "nmu must be >= 1");
+    if (!src_b || !lbc_b) return fail(BURG_EINVAL, "null coefficient table");
+    if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
+    if (snap_every < 1) return fail(BURG_EINVAL, "snap_every must be >= 1");
+    const int64_t ncols = num_steps / snap_every + 1;
+    if (snaps) {
+        if (ld_snaps < ncols)
+            return fail(BURG_EINVAL, "ld_snaps=%lld < %lld columns", (long long)ld_snaps,
+                        (long long)ncols);
+        for (int j = 0; j < nmu; ++j)
+            if (!snaps[j]) return fail(BURG_EINVAL, "null snapshot matrix %d", j);
+    }
+    if (c->engine == BURG_ENGINE_TILES) return fail(BURG_EINVAL, "burg_sweep runs on the pipe engine");
+    if (!c->d_w0) return fail(BURG_ESTATE, "burg_sweep: upload the initial state first");
+    if (int e = stream_setup(c)) return e;
+    if (c->eng_eff != BURG_ENGINE_PIPE)
+        return fail(BURG_ESHAPE, "burg_sweep runs on the pipe engine; this %d x %d grid needs "
+                    "the streaming engine's wider tiles", c->nx, c->nrows);
+    {
+        const int cap = pipe_max_resident_blocks(c->sp.W, true);
+        if (cap < c->sp.nti * c->nwj)
+            return fail(BURG_ESHAPE, "burg_sweep: %d workgroups of the sweep kernel cannot all be "
+                        "resident (%d)", c->sp.nti * c->nwj, cap);
+    }
+    const int W = c->sp.W, T = num_steps;
+    const size_t ncolp = (size_t)c->sp.ntj * W, m = c->m();
+    // per-trajectory coefficient tables (this slab's rows of lbc)
+    double *d_srcb = nullptr, *d_lbcb = nullptr, *d_tr = nullptr;
+    d2 *d_colcb = nullptr;
+    bool registered = false;
+    int rc = BURG_OK;
+    auto cleanup = [&]() {
+        c->sw_T = 0;
+        c->sw_colc = nullptr;
+        c->sw_lbc = nullptr;
+        (void)hipStreamSynchronize(c->stream);
+        if (registered)
+            for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(snaps[j]);
+        dfree(d_srcb);
+        dfree(d_lbcb);
+        dfree(d_colcb);
+        dfree(d_tr);
+    };
+    if ((rc = dalloc(&d_srcb, (size_t)nmu * c->nx)) || (rc = dalloc(&d_lbcb, (size_t)nmu * c->nrows)) ||
+        (rc = dalloc(&d_colcb, (size_t)nmu * ncolp))) {
+        cleanup();
+        return rc;
+    }
+    HIPCHK(hipMemcpyAsync(d_srcb, src_b, sizeof(double) * nmu * c->nx, hipMemcpyHostToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpy2DAsync(d_lbcb, sizeof(double) * c->nrows, lbc_b + c->row0,
+                            sizeof(double) * c->ny_total, sizeof(double) * c->nrows, nmu,
+                            hipMemcpyHostToDevice, c->stream));
+    CHK(launch_colc_batch(c->cf, nmu, d_srcb, (int)ncolp, d_colcb, c->stream));
+
+    // trajectories per launch: as many as the ring budget (a third of free
+    // HBM) holds -- the sweep's states all stay resident until extracted
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    const long long Lmax = (long long)(freeb / 3 / per_entry);
+    long long G = (Lmax - W - 96) / ((long long)T * W);
+    G = std::min<long long>(G, nmu);
+    G = std::min<long long>(G, stream_max_steps(c) / T);
+    G = std::min<long long>(G, kPipeSweepMax);
+    if (const char *e = std::getenv("BURG_SWEEP_GROUP")) {  // test knob: force grouping
+        const long long v = std::atoll(e);
+        if (v > 0) G = std::min(G, v);
+    }
+    if (G < 1) {
+        cleanup();
+        return fail(BURG_ENOMEM, "not enough device memory for one %d-step trajectory ring", T);
+    }
+    const long long L = G * T * W + W + 96;
+    if ((rc = ensure_ring(c, L))) {
+        cleanup();
+        return rc;
+    }
+    int S = 0;
+    if (snaps) {
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        S = (int)std::min<int64_t>(ncols, 64);
+        while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
+        if ((rc = dalloc(&d_tr, (size_t)S * m))) {
+            cleanup();
+            return rc;
+        }
+        registered = true;
+        for (int j = 0; j < nmu; ++j)
+            if (hipHostRegister(snaps[j], m * ld_snaps * sizeof(double), hipHostRegisterDefault) !=
+                hipSuccess) {
+                (void)hipGetLastError();
+                for (int i = 0; i < j; ++i) (void)hipHostUnregister(snaps[i]);
+                registered = false;
+                break;
+            }
+    }
+    float ms = 0.f, flush_ms = 0.f;
+    hipEvent_t f0 = nullptr, f1 = nullptr;
+    (void)hipEventCreate(&f0);
+    (void)hipEventCreate(&f1);
+    stream_stats_begin(c);
+    int64_t launches = 0;
+    int last_nb = 0;
+    for (int g0 = 0; g0 < nmu && rc == BURG_OK; g0 += (int)G) {
+        const int nb = (int)std::min<long long>(G, nmu - g0);
+        if ((rc = launch_ring_load(stream_args(c, L, 0, 0), W, c->d_w0, c->stream))) break;
+        c->sw_T = T;
+        c->sw_colc = d_colcb + (size_t)g0 * ncolp;
+        c->sw_lbc = d_lbcb + (size_t)g0 * c->nrows;
+        rc = stream_launch(c, L, 0, nb * T, &ms);
+        c->sw_T = 0;
+        if (rc) break;
+        ++launches;
+        last_nb = nb;
+        if (!snaps) continue;
+        (void)hipEventRecord(f0, c->stream);
+        for (int j = 0; j < nb && rc == BURG_OK; ++j) {
+            double *dst = snaps[g0 + j];
+            // column 0 = the initial state
+            if (hipMemcpy2DAsync(dst, (size_t)ld_snaps * sizeof(double), c->d_w0, sizeof(double),
+                                 sizeof(double), m, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+                rc = fail(BURG_EHIP, "snapshot copy failed");
+                break;
+            }
+            // columns 1.. = launch states j*T + k*snap_every
+            for (int64_t k0 = 1; k0 < ncols; k0 += S) {
+                const int n = (int)std::min<int64_t>(S, ncols - k0);
+                if (launch_ring_extract(stream_args(c, L, 0, 0), W,
+                                        (int)(j * T + k0 * snap_every), snap_every, n, d_tr, n,
+                                        c->stream) ||
+                    hipMemcpy2DAsync(dst + k0, (size_t)ld_snaps * sizeof(double), d_tr,
+                                     n * sizeof(double), n * sizeof(double), m,
+                                     hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+                    rc = fail(BURG_EHIP, "snapshot extract failed");
+                    break;
+                }
+            }
+        }
+        (void)hipEventRecord(f1, c->stream);
+        (void)hipEventSynchronize(f1);
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, f0, f1);
+        flush_ms += t;
+    }
+    if (rc == BURG_OK) {
+        // the last trajectory's final state becomes the resident state
+        rc = launch_ring_extract(stream_args(c, L, 0, 0), W, last_nb * T, 1, 1,
+                                 c->d_state[c->cur ^ 1], 1, c->stream);
+        if (rc) rc = fail(BURG_EHIP, "ring extract launch failed");
+        else c->cur ^= 1;
+    }
+    if (rc == BURG_OK) rc = stream_stats_end(c, st, (int64_t)nmu * T, launches);
+    if (st) {
+        st->loop_ms = ms;
+        st->flush_ms = flush_ms;
+        st->march_kernel_ms = ms;
+        st->march_launches = launches;
+    }
+    (void)hipEventDestroy(f0);
+    (void)hipEventDestroy(f1);
+    cleanup();
+    return rc;
 }
 
 int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newton_max_its,

@@ -170,10 +170,15 @@ __device__ __forceinline__ void lds_sti(void *p, int v) { *(volatile lds_i32 *)p
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
 
-// LDS image of one workgroup
-template <int W>
+// LDS image of one workgroup (SWEEP: a parameter sweep, burg_sweep -- the
+// initial state and every trajectory's source / inlet terms stay on chip)
+template <int W, bool SWEEP>
 struct PipeLds {
+    static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
     v4u st[4][W][kWave];    // per wave: the lane's outputs of the last W diagonals
+    v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
+    double srcb[kSW][4][W];                        // sweep: src of trajectory j, by column
+    double lbt[kSW][kWave];                        // sweep: inlet term of trajectory j, by row
     v4u cc[4][W];           // per wave: {hx, src} of the tile's columns
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
@@ -182,12 +187,12 @@ struct PipeLds {
     int perm[8];            // [0..3] north grants per wave, [4] east grant of wave 3, [5] abort
 };
 
-template <int W>
+template <int W, bool SWEEP>
 __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
 {
     static_assert(W == 8 || W == 16, "pipe engine: W in {8, 16}");
     constexpr int LW = ilog2<W>();
-    __shared__ PipeLds<W> sm;
+    __shared__ PipeLds<W, SWEEP> sm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
@@ -210,6 +215,21 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     for (int i = threadIdx.x; i < 4 * kRL * W; i += kThreads) (&sm.ins[0][0][0])[i] = lds_empty_g();
     if (threadIdx.x < 8) sm.perm[threadIdx.x] = 0;
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
+    // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
+    const int nsw = SWEEP ? a.K / a.T : 1;
+    if constexpr (SWEEP) {
+        const size_t ncolp = (size_t)ntj * W;
+        for (int i = threadIdx.x; i < nsw * 4 * W; i += kThreads) {
+            const int j = i / (4 * W), kc = i - j * 4 * W;
+            const int kk = kc / W, c = kc - kk * W;
+            (&sm.srcb[0][0][0])[i] = tj0 + kk < ntj ? a.colc_b[j * ncolp + (size_t)(tj0 + kk) * W + c].y
+                                                    : 0.0;
+        }
+        for (int i = threadIdx.x; i < nsw * kWave; i += kThreads) {
+            const int j = i / kWave, l = i - j * kWave;
+            (&sm.lbt[0][0])[i] = a.lbc_b[(size_t)j * ny + ti * kWave + min(l, nrow - 1)];
+        }
+    }
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
         for (int c = lane; c < W; c += kWave) {
@@ -222,7 +242,9 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         for (int c = 0; c < W; ++c) {
             long long e = (a.origin + c + lane - W) % a.L;
             e = e < 0 ? e + a.L : e;
-            sm.st[wave][(c + lane) & (W - 1)][lane] = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
+            const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
+            sm.st[wave][(c + lane) & (W - 1)][lane] = x0;
+            if constexpr (SWEEP) sm.st0[wave][(c + lane) & (W - 1)][lane] = x0;
         }
     }
     __syncthreads();
@@ -352,7 +374,16 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     const int r = ti * kWave + min(lane, top);
     const double ay = a.cf.alpha * a.cf.inv_dy[r];
     const double hy = 0.5 * ay;
-    const double lb = a.cf.lbc[r];
+    // inlet term of the lane's trajectory (sweep: lb of trajectory jl, lb_next
+    // of jl + 1; qn = first step of trajectory jl + 1, whose W columns read
+    // the initial state -- every trajectory starts from w0)
+    double lb = SWEEP ? sm.lbt[0][lane] : a.cf.lbc[r];
+    double lb_next = SWEEP ? sm.lbt[min(1, nsw - 1)][lane] : lb;
+    int qn = SWEEP ? a.T : INT_MAX, jl = 0;
+    // LDS rows of the src table for trajectories jl and jl + 1 (clamped)
+    typedef __attribute__((address_space(3))) const double lds_f64;
+    lds_f64 *src_cur = (lds_f64 *)&sm.srcb[0][k][0];
+    lds_f64 *src_nxt = (lds_f64 *)&sm.srcb[min(1, nsw - 1)][k][0];
     const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
                                              (size_t)a.L * kWave * 16);
     const __amdgpu_buffer_rsrc_t wbox = rsrc(a.wbox, a.wbox_bytes);
@@ -368,6 +399,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     const unsigned ncol = north_dev ? G : 16u;
     v4u(*src_w)[kWave] = k == 0 ? sm.inw : sm.ewe[k - 1];
     v4u *const my_st = &sm.st[k][0][0];
+    v4u *const my_st0 = &sm.st0[k][0][0];
     const long long L = a.L;
     long long pw = a.origin;
     const v4u lempty = lds_empty_g();
@@ -381,6 +413,8 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         v4u xs, cs, gw, gs;
         int pn, pe;
         unsigned ee;
+        bool nt;     // sweep: first step of the lane's next trajectory (state reset)
+        double src;  // sweep: the column's source term of the step's trajectory
     };
     auto fetch = [&](int s) -> In {
         const int t = s - lane;
@@ -389,7 +423,15 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         const bool valid = (unsigned)t < (unsigned)KW;
         const bool need_w = has_west && c == 0 && valid && rowok;
         In in;
-        in.xs = my_st[(s & (W - 1)) * kWave + lane];
+        if constexpr (SWEEP) {
+            in.nt = q >= qn;
+            in.xs = (in.nt ? my_st0 : my_st)[(s & (W - 1)) * kWave + lane];
+            in.src = (in.nt ? src_nxt : src_cur)[c];
+        } else {
+            in.nt = false;
+            in.xs = my_st[(s & (W - 1)) * kWave + lane];
+            in.src = 0.0;
+        }
         in.cs = sm.cc[k][c];
         in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
         in.gs = lds_ld(has_south && s < KW ? &sm.ins[k][(s >> LW) & (kRL - 1)][s & (W - 1)] : &sm.zero);
@@ -419,7 +461,9 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         const d2 co = as_d2(in.cs);
         const double pu = x.x, pv = x.y;
         const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
-        const double sl = (col0_tile && at0) ? co.y + lb : co.y;
+        const double lbu = SWEEP && in.nt ? lb_next : lb;
+        const double srcc = SWEEP ? in.src : co.y;
+        const double sl = (col0_tile && at0) ? srcc + lbu : srcc;
         MarchCell::Pre p;
         p.hx = hx;
         const double hu = 0.5 * pu;
@@ -429,7 +473,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         p.ygp = ay * ((0.5 * pv) * pv);
         p.bu = ((pu - p.xfp) - p.yhp) + sl;
         p.bv = (pv - p.ygp) - p.xhp;
-        const MarchCell::Row rw{ay, hy, lb};
+        const MarchCell::Row rw{ay, hy, lbu};
         // ---- wait until inputs are deposited and outbound slots are granted
         auto blocked = [&](const In &v) -> bool {
             bool b = (need_w && !l_is_data(v.gw)) || (lane == 0 && need_s && !l_is_data(v.gs));
@@ -501,6 +545,18 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         // consumed inbound slots back to empty
         if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
         if (need_s && lane == 0) lds_st(&sm.ins[k][(s >> LW) & (kRL - 1)][s & (W - 1)], lempty);
+        if constexpr (SWEEP) {
+            // the lane finished the first step of its next trajectory: switch
+            if (in.nt && atE) {
+                ++jl;
+                qn += a.T;
+                lb = lb_next;
+                src_cur = src_nxt;
+                const int jn = min(jl + 1, nsw - 1);
+                lb_next = sm.lbt[jn][lane];
+                src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
+            }
+        }
         in = fetch(s + 1);
     }
     if (lane == 0) {
@@ -521,13 +577,16 @@ __global__ void pipe_fill_kernel(v4u *p, size_t n, int color)
 
 bool pipe_width_supported(int W) { return W == 8 || W == 16; }
 
-int pipe_max_resident_blocks(int W)
+// resident workgroups of the pipe kernel (sweep = the burg_sweep variant,
+// whose larger LDS image must also fit one workgroup per CU)
+int pipe_max_resident_blocks(int W, bool sweep)
 {
     int dev = 0, n = 0, ncu = 0;
     if (hipGetDevice(&dev) != hipSuccess) return -3;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return -3;
-    const void *fn = W == 8 ? (const void *)pipe_kernel<8> : (const void *)pipe_kernel<16>;
+    const void *fn = W == 8 ? (sweep ? (const void *)pipe_kernel<8, true> : (const void *)pipe_kernel<8, false>)
+                            : (sweep ? (const void *)pipe_kernel<16, true> : (const void *)pipe_kernel<16, false>);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, 0) != hipSuccess) return -3;
     return n * ncu;
 }
@@ -535,10 +594,16 @@ int pipe_max_resident_blocks(int W)
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
 {
     const int blocks = a.nti * a.nwj;
-    if (W == 8)
-        hipLaunchKernelGGL(pipe_kernel<8>, dim3(blocks), dim3(kThreads), 0, st, a);
+    const bool sweep = a.colc_b != nullptr;
+    if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
+    if (W == 8 && !sweep)
+        hipLaunchKernelGGL((pipe_kernel<8, false>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else if (W == 8)
+        hipLaunchKernelGGL((pipe_kernel<8, true>), dim3(blocks), dim3(kThreads), 0, st, a);
+    else if (W == 16 && !sweep)
+        hipLaunchKernelGGL((pipe_kernel<16, false>), dim3(blocks), dim3(kThreads), 0, st, a);
     else if (W == 16)
-        hipLaunchKernelGGL(pipe_kernel<16>, dim3(blocks), dim3(kThreads), 0, st, a);
+        hipLaunchKernelGGL((pipe_kernel<16, true>), dim3(blocks), dim3(kThreads), 0, st, a);
     else
         return -1;
     return hipGetLastError() == hipSuccess ? 0 : -3;

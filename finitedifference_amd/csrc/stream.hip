@@ -387,6 +387,18 @@ __global__ void colc_kernel(Coeffs cf, d2 *colc, int ncols_pad)
     colc[c] = d2{0.5 * ax, cf.src[cc]};
 }
 
+// sweep table: {hx, src_j} per trajectory j and (padded) column, hx as colc_kernel
+__global__ void colc_batch_kernel(Coeffs cf, const double *src_b, d2 *colc_b, int ncols_pad,
+                                  int nb)
+{
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int j = blockIdx.y;
+    if (c >= ncols_pad || j >= nb) return;
+    const int cc = min(c, cf.nx - 1);
+    const double ax = cf.alpha * cf.inv_dx[cc];
+    colc_b[(size_t)j * ncols_pad + c] = d2{0.5 * ax, src_b[(size_t)j * cf.nx + cc]};
+}
+
 __global__ void fill_sent_kernel(d2 *p, size_t n)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -537,6 +549,14 @@ int launch_colc(const Coeffs &cf, int ncols_pad, void *colc, hipStream_t st)
 {
     hipLaunchKernelGGL(colc_kernel, dim3((ncols_pad + 255) / 256), dim3(256), 0, st, cf,
                        (d2 *)colc, ncols_pad);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_colc_batch(const Coeffs &cf, int nb, const double *src_b, int ncols_pad, void *colc_b,
+                      hipStream_t st)
+{
+    hipLaunchKernelGGL(colc_batch_kernel, dim3((ncols_pad + 255) / 256, nb), dim3(256), 0, st, cf,
+                       src_b, (d2 *)colc_b, ncols_pad, nb);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

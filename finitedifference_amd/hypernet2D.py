@@ -98,6 +98,28 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     return snaps
 
 
+def inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps, mus, *, snap_every=1,
+                                      device=0, verbose=1, allow_nonsquare=False,
+                                      return_stats=False):
+    """inviscid_burgers_implicit2D (C/hypernet2D.py:72-131) for a LIST of mu at
+    once -- what the reference's drivers do one call at a time when they fill
+    a snapshot set (C/run_prom.py:59-71 over the 9 get_snapshot_params,
+    C/run_tests.py:38-49 over 3 test mu).  All trajectories start from w0,
+    run back to back in one pipelined launch on the GPU (burg_sweep) and are
+    each bit-identical to inviscid_burgers_implicit2D(..., mu) with the march
+    solver.  Returns a list of snapshot matrices, one per mu."""
+    mus = [tuple(mu) for mu in mus]
+    if verbose:
+        for mu in mus:
+            print("Running HDM for mu1={}".format(mu[0]))
+    ctx = _ctx_for(grid_x, grid_y, dt, mus[0], device, allow_nonsquare, engine="pipe")
+    snaps, stats = ctx.sweep(mus, int(num_steps), w0=np.asarray(w0, dtype=np.float64).ravel(),
+                             snap_every=int(snap_every))
+    if return_stats:
+        return snaps, stats
+    return snaps
+
+
 def inviscid_burgers_res2D_alt(w, grid_x, grid_y, dt, wp, mu, JDxec=None, JDyec=None, *,
                                device=0):
     """FOM residual R(w; wp, mu) (C/hypernet2D.py:2512-2570), computed on the GPU.
@@ -211,3 +233,34 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
         print("Elapsed time: {:3.3e}".format(time.time() - t0))
         np.save(snap_fn, snaps)
     return snaps
+
+
+def load_or_compute_snaps_sweep(mus, grid_x, grid_y, w0, dt, num_steps,
+                                snap_folder="param_snaps"):
+    """load_or_compute_snaps (C/hypernet2D.py:3111-3145) for a list of mu: the
+    cached ones are loaded, all missing ones are computed in ONE GPU sweep
+    (inviscid_burgers_implicit2D_sweep) and cached under the reference's file
+    names.  Returns the list of snapshot matrices in the order of `mus`."""
+    if not os.path.exists(snap_folder):
+        os.makedirs(snap_folder)
+    saved = get_saved_params(snap_folder=snap_folder)
+    out = [None] * len(mus)
+    todo = []
+    for i, mu in enumerate(mus):
+        fn = param_to_snap_fn(mu, snap_folder=snap_folder)
+        if fn in saved:
+            print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
+            out[i] = np.load(fn)[:, :num_steps + 1]
+        else:
+            todo.append(i)
+    if todo:
+        for i in todo:
+            print(f"Computing new snaps for mu1={mus[i][0]}, mu2={mus[i][1]}")
+        t0 = time.time()
+        snaps = inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps,
+                                                  [mus[i] for i in todo], verbose=0)
+        print("Elapsed time: {:3.3e}".format(time.time() - t0))
+        for i, sn in zip(todo, snaps):
+            np.save(param_to_snap_fn(mus[i], snap_folder=snap_folder), sn)
+            out[i] = sn
+    return out

@@ -84,6 +84,8 @@ class FOMContext:
         if key == self._problem:
             return
         ix, iy, src, lbc = fom_coefficients(grid_x, grid_y, dt, mu, allow_nonsquare)
+        self._grid = (np.asarray(grid_x, dtype=np.float64), np.asarray(grid_y, dtype=np.float64),
+                      float(dt), bool(allow_nonsquare))
         if ix.size != self.nx or iy.size != self.ny_total:
             raise ValueError("grid does not match the context shape")
         _lib.check(self._L.burg_set_problem(self._h, _lib.dptr(ix), _lib.dptr(iy),
@@ -155,6 +157,40 @@ class FOMContext:
         _lib.check(self._L.burg_trajectory(self._h, int(num_steps), 1 if from_initial else 0,
                                            ctypes.byref(st)))
         return st.as_dict()
+
+    def sweep(self, mus, num_steps, w0=None, keep_snaps=True, snap_every=1):
+        """Parameter sweep (burg_sweep): one trajectory of num_steps steps per
+        mu in `mus`, all from w0 (None: the state last passed to upload()),
+        on the grid and dt of the last set_problem, back to back in one
+        pipelined launch per group of trajectories.  Returns (list of snapshot
+        matrices (m, num_steps//snap_every + 1), or None with
+        keep_snaps=False -- then the states stay in HBM --, stats)."""
+        if getattr(self, "_grid", None) is None:
+            raise RuntimeError("set_problem first")
+        gx, gy, dt, nonsq = self._grid
+        mus = [tuple(float(x) for x in mu) for mu in mus]
+        if not mus:
+            raise ValueError("empty mu list")
+        src_b, lbc_b = [], []
+        for mu in mus:
+            _, _, src, lbc = fom_coefficients(gx, gy, dt, mu, nonsq)
+            src_b.append(src)
+            lbc_b.append(lbc)
+        src_b = np.ascontiguousarray(np.stack(src_b))
+        lbc_b = np.ascontiguousarray(np.stack(lbc_b))
+        if w0 is not None:
+            self.upload(w0)
+        ncols = num_steps // snap_every + 1
+        snaps = None
+        ptrs = None
+        if keep_snaps:
+            snaps = [np.zeros((self.m, ncols)) for _ in mus]
+            ptrs = (_lib._D * len(mus))(*[_lib.dptr(a) for a in snaps])
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_sweep(self._h, len(mus), _lib.dptr(src_b), _lib.dptr(lbc_b),
+                                      int(num_steps), ptrs, ncols, int(snap_every),
+                                      ctypes.byref(st)))
+        return snaps, st.as_dict()
 
     def kernel_bench(self, kernel="residual", reps=20):
         """Mean device time (ms) of one launch of the residual or J.x stencil

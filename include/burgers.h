@@ -190,6 +190,23 @@ int burg_kernel_bench(burg_ctx *ctx, int which, int reps, double *avg_ms);
  * stream). */
 int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *stats);
 
+/* Parameter sweep (the reference's snapshot generation over a set of mu,
+ * e.g. C/run_prom.py:59-71 over get_snapshot_params, C/run_tests.py:38-49):
+ * nmu trajectories of num_steps march steps each, all from the uploaded
+ * initial state (burg_upload_state; the reference's w0 is the same for every
+ * mu, C/run_fom.py:33-35), trajectory j with its own coefficients
+ *   src_b[j*nx + c]        = dt*0.02*exp(mu2_j*xc)   (burg_set_problem's src)
+ *   lbc_b[j*ny_total + r]  = 0.5*dt*mu1_j**2/dx[r]   (burg_set_problem's lbc)
+ * (global arrays; a slab context picks its rows).  The trajectories run back
+ * to back in ONE pipelined launch (as many as a third of free HBM holds per
+ * launch), so the pipeline fills once per sweep, not once per trajectory.
+ * Each trajectory is bit-identical to burg_run with that mu.
+ * snaps: NULL (states stay in HBM, benchmark) or nmu host matrices, each
+ * C-order with leading dimension ld_snaps, laid out as burg_run's.  The last
+ * trajectory's final state becomes the resident state.  Pipe engine only. */
+int burg_sweep(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b, int num_steps,
+               double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *stats);
+
 #ifdef __cplusplus
 }
 #endif

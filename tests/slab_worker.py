@@ -9,8 +9,12 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+SWEEP_MUS = [(4.25, 0.015), (5.19, 0.026), (5.5, 0.03)]
+
+
 def main():
     N, T, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    sweep = len(sys.argv) > 4 and sys.argv[4] == "sweep"  # mu sweep (burg_sweep) instead
     import torch.distributed as dist
     from finitedifference_amd.dist import make_slab_context, slab_state
     dist.init_process_group("gloo")
@@ -20,9 +24,15 @@ def main():
     ctx.set_problem(g, g, 0.05, (5.19, 0.026))
     w0 = slab_state(np.ones(2 * N * N), N, N, rank, world)
     dist.barrier()
-    snaps, st, _, _ = ctx.run(w0, T)
-    assert st["engine"] == 2
-    np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
+    if sweep:
+        snaps, st = ctx.sweep(SWEEP_MUS, T, w0=w0)
+        assert st["engine"] == 2
+        for j, sn in enumerate(snaps):
+            np.save(os.path.join(out, f"slab{rank}_mu{j}.npy"), sn)
+    else:
+        snaps, st, _, _ = ctx.run(w0, T)
+        assert st["engine"] == 2
+        np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()

@@ -366,6 +366,36 @@ def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T):
         assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
 
 
+def test_slab_halo_sweep_two_processes_one_gpu(gpu, orc, tmp_path):
+    """The multi-GPU halo stream carries a mu sweep too: 2 slab processes on
+    one GPU, 3 trajectories back to back; each assembled trajectory is the
+    single-grid march for its mu, bit for bit."""
+    import subprocess
+    import sys
+    import socket
+    N, T, world = 128, 6, 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    worker = os.path.join(os.path.dirname(__file__), "slab_worker.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20")
+        procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path),
+                                       "sweep"], env=env))
+    codes = [p.wait(timeout=110) for p in procs]
+    assert codes == [0] * world, codes
+    from finitedifference_amd.dist import assemble_snaps
+    from slab_worker import SWEEP_MUS
+    for j, mu in enumerate(SWEEP_MUS):
+        parts = [np.load(os.path.join(tmp_path, f"slab{r}_mu{j}.npy")) for r in range(world)]
+        snaps = assemble_snaps(parts, N, N)
+        ref, _, _ = orc.Problem(N, mu=mu).fom(np.ones(2 * N * N), T)
+        for k in range(T + 1):
+            assert np.array_equal(snaps[:, k], ref[k]), f"mu {mu} step {k}"
+
+
 def test_trajectory_from_initial_is_repeatable(gpu, orc):
     """burg_trajectory (the bench's unit of work): from the uploaded w0 every
     time, or continuing from the resident state; final states = oracle."""
@@ -380,3 +410,66 @@ def test_trajectory_from_initial_is_repeatable(gpu, orc):
         assert np.array_equal(ctx.download(), ref[T])
     ctx.trajectory(T, from_initial=False)
     assert np.array_equal(ctx.download(), ref[2 * T])
+
+
+# ------------------------------------------------------ parameter sweep --
+SWEEP_MUS = [(4.25, 0.015), (5.19, 0.026), (5.5, 0.03), (4.875, 0.0225), (4.56, 0.019)]
+
+
+@pytest.mark.parametrize("N,ny,W,T,nmu,group", [
+    (64, 64, 16, 5, 3, 0), (130, 70, 8, 4, 5, 2), (96, 200, 16, 3, 4, 0), (40, 64, 8, 9, 2, 1),
+    (136, 136, 0, 6, 12, 0)])
+def test_sweep_each_trajectory_bitwise(gpu, orc, monkeypatch, N, ny, W, T, nmu, group):
+    """burg_sweep: every trajectory of the sweep (own mu, all from w0) is
+    bit-equal to the oracle's sequential march for that mu -- across the
+    state resets and coefficient switches inside one launch, across launch
+    groups (forced small groups; 12 mu > the 10 a launch holds)."""
+    if group:
+        monkeypatch.setenv("BURG_SWEEP_GROUP", str(group))
+    mus = [SWEEP_MUS[i % len(SWEEP_MUS)] for i in range(nmu)]
+    mus = [(m1 + 0.01 * i, m2) for i, (m1, m2) in enumerate(mus)]
+    P0 = orc.Problem(N, ny, Ly=100.0 * ny / N, allow_nonsquare=(N != ny))
+    w0 = state_after(orc, P0, 2)
+    ctx = FOMContext_for(N, ny, engine="pipe", stream_w=W)
+    ctx.set_problem(P0.grid_x, P0.grid_y, P0.dt, P0.mu, allow_nonsquare=(N != ny))
+    snaps, st = ctx.sweep(mus, T, w0=w0)
+    assert st["engine"] == 2 and st["steps"] == nmu * T
+    for mu, sn in zip(mus, snaps):
+        P = orc.Problem(N, ny, mu=mu, Ly=100.0 * ny / N, allow_nonsquare=(N != ny))
+        ref, _, _ = P.fom(w0, T)
+        for j in range(T + 1):
+            assert np.array_equal(sn[:, j], ref[j]), f"mu={mu} step {j}"
+    # the last trajectory's final state is left resident
+    assert np.array_equal(ctx.download(), snaps[-1][:, T])
+
+
+def test_sweep_snap_every_and_resident(gpu, orc):
+    N, T = 64, 9
+    mus = SWEEP_MUS[:3]
+    ctx = make_ctx(N, engine="pipe")
+    w0 = np.ones(ctx.m)
+    full, _ = ctx.sweep(mus, T, w0=w0)
+    sub, _ = ctx.sweep(mus, T, w0=w0, snap_every=3)
+    for a, b in zip(full, sub):
+        assert np.array_equal(a[:, ::3], b)
+    none, st = ctx.sweep(mus, T, w0=w0, keep_snaps=False)
+    assert none is None and st["steps"] == 3 * T
+    assert np.array_equal(ctx.download(), full[-1][:, T])
+
+
+def test_sweep_api_matches_single_runs(gpu, tmp_path):
+    """hypernet2D.load_or_compute_snaps_sweep writes the same cache files
+    (reference names, C/hypernet2D.py:3081-3105) with the same snapshots as
+    one load_or_compute_snaps call per mu."""
+    from finitedifference_amd import hypernet2D as H
+    N, T = 50, 6
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    w0 = np.ones(2 * N * N)
+    mus = SWEEP_MUS[:4]
+    a = H.load_or_compute_snaps_sweep(mus, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "a"))
+    for mu, sa in zip(mus, a):
+        sb = H.load_or_compute_snaps(mu, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "b"))
+        assert np.array_equal(sa, sb)
+    again = H.load_or_compute_snaps_sweep(mus, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "a"))
+    for x, y in zip(a, again):
+        assert np.array_equal(x, y)
