@@ -26,7 +26,7 @@ EXPORTS = (
     "burg_slab_connect", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
-    "burg_kernel_bench", "burg_sweep",
+    "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -119,6 +119,8 @@ def load(path=None):
                                                 ctypes.POINTER(BurgStats)]),
             "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
             "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
+            "burg_ecsw_matrix": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int, _D, _D,
+                                                ctypes.POINTER(BurgStats)]),
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),

@@ -171,6 +171,9 @@ bool pipe_width_supported(int W);
 int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);
+int launch_basis_transpose(const double *b, double *bt, size_t m, int npod, hipStream_t st);
+int launch_ecsw(const Coeffs &cf, const double *w, const double *wp, const double *bt, int npod,
+                double *cblk, hipStream_t st);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
                      int ldo, hipStream_t st);
 

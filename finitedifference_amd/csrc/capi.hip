@@ -1329,6 +1329,81 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
     return rc;
 }
 
+int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const double *prev_states,
+                     int n_pod, const double *basis, double *C, burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (st) std::memset(st, 0, sizeof *st);
+    if (n_snaps < 1 || n_pod < 1) return fail(BURG_EINVAL, "n_snaps and n_pod must be >= 1");
+    if (!states || !prev_states || !basis || !C) return fail(BURG_EINVAL, "null array");
+    if (c->world > 1) return fail(BURG_EINVAL, "burg_ecsw_matrix: single-GPU contexts only");
+    const size_t m = c->m(), n = c->n();
+    const size_t blk = (size_t)n_pod * n;  // one snapshot's C rows
+    double *d_b = nullptr, *d_bt = nullptr, *d_w = nullptr, *d_cb = nullptr;
+    bool registered = false;
+    int rc = BURG_OK;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(c->stream);
+        if (registered) (void)hipHostUnregister(C);
+        dfree(d_b);
+        dfree(d_bt);
+        dfree(d_w);
+        dfree(d_cb);
+    };
+    if ((rc = dalloc(&d_b, m * n_pod)) || (rc = dalloc(&d_bt, m * n_pod)) ||
+        (rc = dalloc(&d_w, 2 * m)) || (rc = dalloc(&d_cb, blk))) {
+        cleanup();
+        return rc;
+    }
+    HIPCHK(hipMemcpyAsync(d_b, basis, sizeof(double) * m * n_pod, hipMemcpyHostToDevice,
+                          c->stream));
+    CHK(launch_basis_transpose(d_b, d_bt, m, n_pod, c->stream));
+    registered = hipHostRegister(C, sizeof(double) * blk * n_snaps, hipHostRegisterDefault) ==
+                 hipSuccess;
+    (void)hipGetLastError();
+    float kern = 0.f, copy = 0.f;
+    hipEvent_t e2 = nullptr;
+    (void)hipEventCreate(&e2);
+    for (int i = 0; i < n_snaps && rc == BURG_OK; ++i) {
+        if (hipMemcpyAsync(d_w, states + (size_t)i * m, sizeof(double) * m, hipMemcpyHostToDevice,
+                           c->stream) != hipSuccess ||
+            hipMemcpyAsync(d_w + m, prev_states + (size_t)i * m, sizeof(double) * m,
+                           hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+            rc = fail(BURG_EHIP, "state upload failed");
+            break;
+        }
+        (void)hipEventRecord(c->ev0, c->stream);
+        if (launch_ecsw(c->cf, d_w, d_w + m, d_bt, n_pod, d_cb, c->stream)) {
+            rc = fail(BURG_EHIP, "ecsw kernel launch failed");
+            break;
+        }
+        (void)hipEventRecord(c->ev1, c->stream);
+        if (hipMemcpyAsync(C + (size_t)i * blk, d_cb, sizeof(double) * blk,
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+            rc = fail(BURG_EHIP, "C block copy failed");
+            break;
+        }
+        (void)hipEventRecord(e2, c->stream);
+        if (hipEventSynchronize(e2) != hipSuccess) {
+            rc = fail(BURG_EHIP, "ecsw: %s", hipGetErrorString(hipGetLastError()));
+            break;
+        }
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, c->ev0, c->ev1);
+        kern += t;
+        (void)hipEventElapsedTime(&t, c->ev1, e2);
+        copy += t;
+    }
+    (void)hipEventDestroy(e2);
+    if (st) {
+        st->loop_ms = kern;
+        st->flush_ms = copy;
+        st->steps = n_snaps;
+    }
+    cleanup();
+    return rc;
+}
+
 int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newton_max_its,
              double newton_rtol, double *snaps, int64_t ld_snaps, int snap_every,
              burg_stats *st, int32_t *step_iters, double *step_rel)

@@ -193,6 +193,21 @@ def newton_raphson(func, jac, x0, max_its=20, relnorm_cutoff=1e-12):
     return x, resnorms
 
 
+def compute_ECSW_training_matrix_2D(snaps, prev_snaps, basis, res=None, jac=None, grid_x=None,
+                                    grid_y=None, dt=None, mu=None, *, device=0):
+    """ECSW hyper-reduction training matrix (C/hypernet2D.py:2719-2740), same
+    signature and (n_pod*n_snaps, n_hdm) result, assembled on the GPU in one
+    kernel per snapshot (residual + J(snap) @ basis + the per-node products).
+    `res` / `jac` are accepted for call compatibility: the reference passes
+    inviscid_burgers_res2D and inviscid_burgers_exact_jac2D, which the kernel
+    computes (the residual in res2D_alt's op order, equal to res2D's to
+    round-off)."""
+    if grid_x is None or grid_y is None or dt is None or mu is None:
+        raise ValueError("grid_x, grid_y, dt and mu are required")
+    ctx = _ctx_for(grid_x, grid_y, dt, mu, device)
+    return ctx.ecsw_matrix(snaps, prev_snaps, basis)
+
+
 def compute_error(rom_snaps, hdm_snaps):
     """Relative error at each time step (C/hypernet2D.py:3074-3079)."""
     sq_hdm = np.sqrt(np.square(rom_snaps).sum(axis=0))

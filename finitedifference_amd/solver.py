@@ -192,6 +192,26 @@ class FOMContext:
                                       ctypes.byref(st)))
         return snaps, st.as_dict()
 
+    def ecsw_matrix(self, snaps, prev_snaps, basis, return_stats=False):
+        """ECSW training matrix (burg_ecsw_matrix) of snapshot columns
+        snaps[:, i] with previous states prev_snaps[:, i] and a (2n, npod)
+        basis, on the problem of the last set_problem: (npod*nsnaps, n)."""
+        snaps = np.asarray(snaps, dtype=np.float64)
+        prev_snaps = np.asarray(prev_snaps, dtype=np.float64)
+        if snaps.ndim != 2 or snaps.shape[0] != self.m or prev_snaps.shape != snaps.shape:
+            raise ValueError("snaps / prev_snaps must be (2*nx*ny, n_snaps) and equal in shape")
+        basis = np.ascontiguousarray(np.asarray(basis, dtype=np.float64))
+        if basis.ndim != 2 or basis.shape[0] != self.m:
+            raise ValueError("basis must be (2*nx*ny, n_pod)")
+        ns, npod = snaps.shape[1], basis.shape[1]
+        states = np.ascontiguousarray(snaps.T)  # state-major: column i contiguous
+        prev = np.ascontiguousarray(prev_snaps.T)
+        C = np.zeros((npod * ns, self.m // 2))
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_ecsw_matrix(self._h, ns, _lib.dptr(states), _lib.dptr(prev), npod,
+                                            _lib.dptr(basis), _lib.dptr(C), ctypes.byref(st)))
+        return (C, st.as_dict()) if return_stats else C
+
     def kernel_bench(self, kernel="residual", reps=20):
         """Mean device time (ms) of one launch of the residual or J.x stencil
         on device-resident operands (burg_kernel_bench; upload() first)."""

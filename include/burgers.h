@@ -15,6 +15,9 @@
  *                       (+ np.linalg.norm of it, :1831/:1839)
  *   burg_jvp            C/hypernet2D.py:2627-2656 inviscid_burgers_exact_jac2D(w) @ x
  *   burg_block_solve    C/hypernet2D.py:1854      spsolve(J(w), rhs)
+ *   burg_sweep          a loop of inviscid_burgers_implicit2D over a mu set
+ *                       (C/run_prom.py:59-71, C/run_tests.py:38-49)
+ *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
  *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
  *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
  *
@@ -206,6 +209,19 @@ int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *
  * trajectory's final state becomes the resident state.  Pipe engine only. */
 int burg_sweep(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b, int num_steps,
                double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *stats);
+
+/* ECSW hyper-reduction training matrix (compute_ECSW_training_matrix_2D,
+ * C/hypernet2D.py:2719-2740), with the context's problem (grid, dt, mu of
+ * burg_set_problem):
+ *   C[isnap*n_pod + k, node] = R_u[node] W_u[node,k] + R_v[node] W_v[node,k],
+ *   R = residual(states[isnap]; prev_states[isnap]), W = J(states[isnap]) basis.
+ * states, prev_states: n_snaps states of 2n doubles each, state-major (the
+ * columns of the reference's snapshot blocks, contiguous); basis: (2n x n_pod)
+ * C-order (the reference's basis array); C: (n_pod*n_snaps x n) C-order
+ * output, n = nx*ny.  stats (may be NULL): loop_ms = kernel time, flush_ms =
+ * D2H time of C, steps = n_snaps.  Single-GPU contexts. */
+int burg_ecsw_matrix(burg_ctx *ctx, int n_snaps, const double *states, const double *prev_states,
+                     int n_pod, const double *basis, double *C, burg_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -125,6 +125,27 @@ class Problem:
                       _p(snaps), its.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), _p(rel))
         return snaps, its, rel
 
+    def ecsw_matrix(self, snaps, prev_snaps, basis):
+        """compute_ECSW_training_matrix_2D (C/hypernet2D.py:2719-2740) restated:
+        per snapshot column, the residual R(snap; prev) and W = J(snap) @ basis
+        column by column (orc_residual / orc_jvp), then
+        C[isnap*npod + k, node] = R_u[node] W_u[node, k] + R_v[node] W_v[node, k]
+        (the reference's inner loop, :2737-2738).  Column-major snapshots as in
+        the reference; the residual follows res2D_alt's op order (the reference
+        passes res2D, :2468-2510, equal to 4.4e-16)."""
+        snaps = np.asarray(snaps, dtype=np.float64)
+        prev_snaps = np.asarray(prev_snaps, dtype=np.float64)
+        basis = np.asarray(basis, dtype=np.float64)
+        m, ns = snaps.shape
+        n = m // 2
+        npod = basis.shape[1]
+        C = np.zeros((npod * ns, n))
+        for i in range(ns):
+            r = self.residual(snaps[:, i], prev_snaps[:, i])
+            Wi = np.stack([self.jvp(snaps[:, i], basis[:, k]) for k in range(npod)], axis=1)
+            C[i * npod:(i + 1) * npod, :] = (r[:n, None] * Wi[:n] + r[n:, None] * Wi[n:]).T
+        return C
+
 
 def rel_l2(a, b):
     a, b = np.asarray(a), np.asarray(b)

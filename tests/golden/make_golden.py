@@ -23,6 +23,10 @@ Fixtures written
   ref_fine750.npz    F/ grid 750^2, first 2 steps at mu=(5.19, 0.026)
   author_pickles.npz HDM mid-line slices byte-scanned (never unpickled) from
                      the author's C/ and F/ predict_mu_5.19e+00_2.60e-02_hprom.pickle
+  ref_ecsw.npz       compute_ECSW_training_matrix_2D (:2719-2740) with the
+                     reference's own callbacks (res2D, exact_jac2D) on
+                     reference snapshots, the driver's 3-step offset sampling
+                     (C/run_HPROM_ecsw_joshua_.py:81-84) and a POD basis
   author_logs.json   Newton counts/residuals from the author's SLURM log
                      F/output_55034725.log (750^2)
 """
@@ -129,6 +133,23 @@ def make_ops(hn):
                         f"{tag}_jx_norm": np.linalg.norm(jx), f"{tag}_jx_at": jx[idx]})
         print(f"ops N={N} done")
     np.savez_compressed(os.path.join(HERE, "ref_ops.npz"), **out)
+
+
+def make_ecsw(hn):
+    out = {}
+    for tag, N, T, mu, npod, f in (("n16", 16, 14, (4.56, 0.019), 6, 2),
+                                   ("n24", 24, 10, (5.19, 0.026), 5, 3)):
+        gx, gy = hn.make_2D_grid(0, 100, 0, 100, N, N)
+        snaps, _, _ = run_reference(hn, N, T, mu)
+        basis = np.linalg.svd(snaps, full_matrices=False)[0][:, :npod]
+        s_use, s_prev = snaps[:, 3:T:f], snaps[:, 0:T - 3:f]
+        C = hn.compute_ECSW_training_matrix_2D(s_use, s_prev, basis, hn.inviscid_burgers_res2D,
+                                               hn.inviscid_burgers_exact_jac2D, gx, gy, 0.05,
+                                               list(mu))
+        out.update({f"{tag}_snaps": snaps, f"{tag}_basis": basis, f"{tag}_C": C,
+                    f"{tag}_meta": np.array([N, T, mu[0], mu[1], 0.05, npod, f])})
+        print(f"ecsw {tag}: C {C.shape}")
+    np.savez_compressed(os.path.join(HERE, "ref_ecsw.npz"), **out)
 
 
 def _summaries(snaps, N, steps_full):
@@ -252,6 +273,8 @@ def main():
             make_small(hn)
         if not only or "ops" in only:
             make_ops(hn)
+        if not only or "ecsw" in only:
+            make_ecsw(hn)
         if not only or "coarse" in only:
             make_coarse250(hn, args.coarse_npy, args.coarse_log)
         if (not only or "fine" in only) and not args.skip_750:

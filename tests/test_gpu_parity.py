@@ -473,3 +473,36 @@ def test_sweep_api_matches_single_runs(gpu, tmp_path):
     again = H.load_or_compute_snaps_sweep(mus, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "a"))
     for x, y in zip(a, again):
         assert np.array_equal(x, y)
+
+
+# ------------------------------------------------ ECSW training matrix --
+@pytest.mark.parametrize("tag", ["n16", "n24"])
+def test_ecsw_matrix_vs_reference_and_oracle(gpu, orc, tag):
+    """compute_ECSW_training_matrix_2D on the GPU (burg_ecsw_matrix): bit-equal
+    to the oracle restatement and within round-off of the reference's own
+    output (its res2D / exact_jac2D callbacks, the driver's offset sampling)."""
+    from finitedifference_amd import hypernet2D as H
+    g = golden("ref_ecsw.npz")
+    N, T, m1, m2, dt, npod, f = g[f"{tag}_meta"]
+    N, T, f = int(N), int(T), int(f)
+    sn, basis = g[f"{tag}_snaps"], g[f"{tag}_basis"]
+    s_use, s_prev = sn[:, 3:T:f], sn[:, 0:T - 3:f]
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    C = H.compute_ECSW_training_matrix_2D(s_use, s_prev, basis, None, None, gx, gy, dt, (m1, m2))
+    P = orc.Problem(N, mu=(m1, m2), dt=dt)
+    assert np.array_equal(C, P.ecsw_matrix(s_use, s_prev, basis))
+    assert rel(C, g[f"{tag}_C"]) <= 1e-14
+
+
+def test_ecsw_matrix_multiblock_bitwise(gpu, orc):
+    """Several 256-column blocks, ragged last block, many basis vectors."""
+    N, ns, npod = 300, 3, 17
+    P = orc.Problem(N)
+    rng = np.random.default_rng(1234557)
+    snaps = rng.uniform(1.0, 6.0, (P.m, ns))
+    prev = rng.uniform(1.0, 6.0, (P.m, ns))
+    basis = np.linalg.qr(rng.standard_normal((P.m, npod)))[0]
+    ctx = make_ctx(N)
+    C, st = ctx.ecsw_matrix(snaps, prev, basis, return_stats=True)
+    assert C.shape == (npod * ns, N * N) and st["steps"] == ns
+    assert np.array_equal(C, P.ecsw_matrix(snaps, prev, basis))

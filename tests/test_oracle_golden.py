@@ -182,3 +182,20 @@ def test_tile_schedule_converges_in_few_passes(orc):
     ws, k, done = P.march_tiled(w, tw=64, tol=2.0 ** -50)
     assert k <= 6
     assert rel(ws, P.march_step(w)) <= 1e-15
+
+
+def test_oracle_ecsw_matrix_vs_reference():
+    """Oracle restatement of compute_ECSW_training_matrix_2D (C/hypernet2D.py:
+    2719-2740) against the reference's own output (tests/golden/ref_ecsw.npz,
+    generated by importing the reference: make_golden.py --only ecsw)."""
+    from oracle import oracle
+    g = golden("ref_ecsw.npz")
+    for tag in ("n16", "n24"):
+        N, T, m1, m2, dt, npod, f = g[f"{tag}_meta"]
+        N, T, f = int(N), int(T), int(f)
+        P = oracle.Problem(N, mu=(m1, m2), dt=dt)
+        sn = g[f"{tag}_snaps"]
+        C = P.ecsw_matrix(sn[:, 3:T:f], sn[:, 0:T - 3:f], g[f"{tag}_basis"])
+        ref = g[f"{tag}_C"]
+        assert C.shape == ref.shape == (int(npod) * len(range(3, T, f)), N * N)
+        assert np.linalg.norm(C - ref) <= 1e-14 * np.linalg.norm(ref)
