@@ -40,42 +40,67 @@ __global__ __launch_bounds__(256) void basis_transpose_kernel(const double *__re
     }
 }
 
+// lane i <- lane i-1 (wave shift); lane 0 keeps `old0`
+__device__ __forceinline__ double shr1(double old0, double x)
+{
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(old0), __double2loint(x), 0x138,
+                                               0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old0), __double2hiint(x), 0x138,
+                                               0xf, 0xf, false);
+    return __hiloint2double(hi, lo);
+}
+
+// A workgroup: 256 columns x kER rows x one group of basis vectors
+// (blockIdx.z; k = z, z + gridDim.z, ...).  The node's state, residual and
+// neighbour states are computed once into registers; then per basis vector
+// each cell loads only its own (xu, xv): the south pair is the previous
+// row's (carried), the west pair the left lane's (DPP; lane 0 loads it).
+constexpr int kER = 4;
+
 __global__ __launch_bounds__(kEB) void ecsw_kernel(Coeffs cf, const double *__restrict__ w,
                                                    const double *__restrict__ wp,
                                                    const double *__restrict__ bt, int npod,
                                                    double *__restrict__ cblk)
 {
-    const int nx = cf.nx;
-    const size_t n = (size_t)nx * cf.ny;
+    const int nx = cf.nx, ny = cf.ny;
+    const size_t n = (size_t)nx * ny;
     const int c = blockIdx.x * kEB + threadIdx.x;
-    const int r = blockIdx.y;
-    if (c >= nx) return;
-    const size_t i = (size_t)r * nx + c;
+    const int r0 = blockIdx.y * kER;
+    const int nr = min(kER, ny - r0);
+    const bool colok = c < nx;
+    const int cc = colok ? c : nx - 1;  // padding lanes mirror a real column, store nothing
+    const bool lane0 = (threadIdx.x & (kWave - 1)) == 0;
+    const bool west = c > 0;
     const double a = cf.alpha;
+    const double ax = a * cf.inv_dx[cc];
+    const double axw = west ? a * cf.inv_dx[cc - 1] : 0.0;
     const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
-    const double ay = a * cf.inv_dy[r];
-    const double ax = a * cf.inv_dx[c];
-    const bool west = c > 0, south = r > 0;
-    const double axw = west ? a * cf.inv_dx[c - 1] : 0.0;
-    const double ays = south ? a * cf.inv_dy[r - 1] : 0.0;
-    const size_t iw = west ? i - 1 : i, is = south ? i - nx : i;
-    const double ui = u[i], vi = v[i];
-    const double uW = u[iw], vW = v[iw], uS = u[is], vS = v[is];
 
-    // ---- residual (stencil.hip residual_kernel / orc_residual op order)
-    double ru, rv;
-    {
+    double U[kER], V[kER], UW[kER], VW[kER], US[kER], VS[kER], RU[kER], RV[kER], AY[kER],
+        AYS[kER];
+#pragma unroll
+    for (int rr = 0; rr < kER; ++rr) {
+        if (rr >= nr) break;
+        const int r = r0 + rr;
+        const size_t i = (size_t)r * nx + cc;
+        const bool south = r > 0;
+        const size_t iw = west ? i - 1 : i, is = south ? i - nx : i;
+        const double ui = u[i], vi = v[i];
+        const double uW = u[iw], vW = v[iw], uS = u[is], vS = v[is];
+        const double ay = a * cf.inv_dy[r];
+        const double ays = south ? a * cf.inv_dy[r - 1] : 0.0;
+        // residual (stencil.hip residual_kernel / orc_residual op order)
         const double upi = up[i], vpi = vp[i];
         const double Su = 0.5 * (ui * ui) + 0.5 * (upi * upi);
         const double Sv = 0.5 * (vi * vi) + 0.5 * (vpi * vpi);
         const double Suv = (0.5 * ui) * vi + (0.5 * upi) * vpi;
-        double dxu = ax * Su, dyuv = ay * Suv, dyv = ay * Sv, dxuv = cf.inv_dx[c] * Suv;
+        double dxu = ax * Su, dyuv = ay * Suv, dyv = ay * Sv, dxuv = cf.inv_dx[cc] * Suv;
         if (west) {
             const double upj = up[iw], vpj = vp[iw];
             const double SuW = 0.5 * (uW * uW) + 0.5 * (upj * upj);
             const double SuvW = (0.5 * uW) * vW + (0.5 * upj) * vpj;
             dxu = dxu + (-axw) * SuW;
-            dxuv = dxuv + (-cf.inv_dx[c - 1]) * SuvW;
+            dxuv = dxuv + (-cf.inv_dx[cc - 1]) * SuvW;
         }
         if (south) {
             const double upS = up[is], vpS = vp[is];
@@ -84,35 +109,61 @@ __global__ __launch_bounds__(kEB) void ecsw_kernel(Coeffs cf, const double *__re
             dyuv = dyuv + (-ays) * SuvS;
             dyv = dyv + (-ays) * SvS;
         }
-        ru = ui - upi;
+        double ru = ui - upi;
         ru = ru + dxu;
         ru = ru + dyuv;
-        ru = ru - cf.src[c];
+        ru = ru - cf.src[cc];
         ru = ru - (c == 0 ? cf.lbc[r] : 0.0);
-        rv = vi - vpi;
+        double rv = vi - vpi;
         rv = rv + dyv;
         rv = rv + a * dxuv;
+        U[rr] = ui, V[rr] = vi, UW[rr] = uW, VW[rr] = vW, US[rr] = uS, VS[rr] = vS;
+        RU[rr] = ru, RV[rr] = rv, AY[rr] = ay, AYS[rr] = ays;
     }
-    // ---- J(w) basis_k at this node (stencil.hip jvp / orc_jvp op order)
-    for (int k = 0; k < npod; ++k) {
+    const bool wl = lane0 && west;
+    for (int k = blockIdx.z; k < npod; k += gridDim.z) {
         const double *xu = bt + (size_t)k * 2 * n, *xv = xu + n;
-        const double xui = xu[i], xvi = xv[i];
-        const double m = vi * xui + ui * xvi;
-        double yu = xui + ax * ui * xui + 0.5 * ay * m;
-        double yv = xvi + ay * vi * xvi + 0.5 * ax * m;
-        if (west) {
-            const double xuj = xu[iw], xvj = xv[iw];
-            const double mW = vW * xuj + uW * xvj;
-            yu -= axw * uW * xuj;
-            yv -= 0.5 * axw * mW;
+        double xuS = 0.0, xvS = 0.0;
+        if (r0 > 0) {
+            const size_t is = (size_t)(r0 - 1) * nx + cc;
+            xuS = xu[is], xvS = xv[is];
         }
-        if (south) {
-            const double xuj = xu[is], xvj = xv[is];
-            const double mS = vS * xuj + uS * xvj;
-            yu -= 0.5 * ays * mS;
-            yv -= ays * vS * xvj;
+        double XU[kER], XV[kER], XUW[kER], XVW[kER];
+#pragma unroll
+        for (int rr = 0; rr < kER; ++rr) {
+            if (rr >= nr) break;
+            const size_t i = (size_t)(r0 + rr) * nx + cc;
+            const size_t j = wl ? i - 1 : i;
+            XU[rr] = xu[i], XV[rr] = xv[i], XUW[rr] = xu[j], XVW[rr] = xv[j];
         }
-        __builtin_nontemporal_store(ru * yu + rv * yv, &cblk[(size_t)k * n + i]);
+#pragma unroll
+        for (int rr = 0; rr < kER; ++rr) {
+            if (rr >= nr) break;
+            const int r = r0 + rr;
+            const size_t i = (size_t)r * nx + cc;
+            const double ui = U[rr], vi = V[rr], xui = XU[rr], xvi = XV[rr];
+            const double xuj = shr1(XUW[rr], xui), xvj = shr1(XVW[rr], xvi);
+            // J(w) basis_k at the node (stencil.hip jvp / orc_jvp op order)
+            const double ay = AY[rr], ays = AYS[rr];
+            const double m = vi * xui + ui * xvi;
+            double yu = xui + ax * ui * xui + 0.5 * ay * m;
+            double yv = xvi + ay * vi * xvi + 0.5 * ax * m;
+            if (west) {
+                const double uW = UW[rr], vW = VW[rr];
+                const double mW = vW * xuj + uW * xvj;
+                yu -= axw * uW * xuj;
+                yv -= 0.5 * axw * mW;
+            }
+            if (r > 0) {
+                const double uS = US[rr], vS = VS[rr];
+                const double mS = vS * xuS + uS * xvS;
+                yu -= 0.5 * ays * mS;
+                yv -= ays * vS * xvS;
+            }
+            if (colok) __builtin_nontemporal_store(RU[rr] * yu + RV[rr] * yv, &cblk[(size_t)k * n + i]);
+            xuS = xui;
+            xvS = xvi;
+        }
     }
 }
 
@@ -128,8 +179,12 @@ int launch_basis_transpose(const double *b, double *bt, size_t m, int npod, hipS
 int launch_ecsw(const Coeffs &cf, const double *w, const double *wp, const double *bt, int npod,
                 double *cblk, hipStream_t st)
 {
-    const dim3 grid((unsigned)((cf.nx + kEB - 1) / kEB), (unsigned)cf.ny);
-    hipLaunchKernelGGL(ecsw_kernel, grid, dim3(kEB), 0, st, cf, w, wp, bt, npod, cblk);
+    const unsigned gx = (unsigned)((cf.nx + kEB - 1) / kEB), gy = (unsigned)((cf.ny + kER - 1) / kER);
+    // basis-vector groups: enough workgroups to fill the chip (>= 2048)
+    unsigned gz = 1;
+    while (gz < (unsigned)npod && (size_t)gx * gy * gz < 2048) gz *= 2;
+    gz = gz > (unsigned)npod ? (unsigned)npod : gz;
+    hipLaunchKernelGGL(ecsw_kernel, dim3(gx, gy, gz), dim3(kEB), 0, st, cf, w, wp, bt, npod, cblk);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
