@@ -65,6 +65,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stencil-nx", type=int, default=8192,
                     help="grid of the residual / J.x roofline probe (0: skip)")
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N > 1 rehearsal on a one-GPU box: every rank on device 0, gloo "
+                         "for the host-side collectives (use small slabs so all ranks' "
+                         "workgroups are resident together)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     return ap.parse_args()
 
@@ -150,10 +154,15 @@ def main():
     import torch.distributed as dist
     from finitedifference_amd.dist import make_slab_context
 
+    rehearse = world > 1 and args.rehearse_one_gpu
+    dev = 0 if rehearse else local
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    ctx = make_slab_context(nx, ny, rank, world, device=local if world > 1 else 0,
+        torch.cuda.set_device(dev)
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    ctx = make_slab_context(nx, ny, rank, world, device=dev if world > 1 else 0,
                             dist=dist if world > 1 else None, engine=args.engine,
                             stream_w=args.stream_w)
     gx = np.linspace(0, 100, nx + 1)
@@ -189,7 +198,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     cells = nx * ny  # whole job
