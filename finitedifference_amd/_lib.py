@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -26,7 +26,7 @@ EXPORTS = (
     "burg_slab_connect", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
-    "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix",
+    "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_lspg",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -121,6 +121,10 @@ def load(path=None):
             "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
             "burg_ecsw_matrix": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int, _D, _D,
                                                 ctypes.POINTER(BurgStats)]),
+            "burg_lspg": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int,
+                                         ctypes.c_double, ctypes.c_double, _D, ctypes.c_int64,
+                                         _D, ctypes.c_int64, _I32, _D, _D,
+                                         ctypes.POINTER(BurgStats)]),
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),

@@ -174,6 +174,27 @@ int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);
 int launch_basis_transpose(const double *b, double *bt, size_t m, int npod, hipStream_t st);
 int launch_ecsw(const Coeffs &cf, const double *w, const double *wp, const double *bt, int npod,
                 double *cblk, hipStream_t st);
+// LSPG PROM (lspg.hip): at most kLspgMaxPod POD vectors (the augmented
+// Gram matrix [JV | -R]^T [JV | -R] is at most 128 x 128)
+constexpr int kLspgMaxPod = 127;
+struct LspgArgs {
+    Coeffs cf;           // square grid (nx == ny), single domain
+    const double *w;     // state (2n)
+    const double *wT;    // state, each plane transposed (2n)
+    const double *bt;    // basis, (npod, 2n)
+    const double *btT;   // basis, (npod, 2n), each plane transposed
+    const double *r;     // residual R(w; wp) (2n)
+    int npod;
+};
+int lspg_cols(int npod);
+size_t lspg_partial_count(int nx, int npod);
+int launch_lspg_expand(const double *bt, const double *y, int npod, size_t m, double *w,
+                       hipStream_t st);
+int launch_lspg_project(const double *bt, const double *x, int npod, size_t m, double *scratch,
+                        double *y, hipStream_t st);
+int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t st);
+int launch_lspg_solve(const double *G, int npod, double *y, double *dy, unsigned *err,
+                      hipStream_t st);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
                      int ldo, hipStream_t st);
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1544,6 +1545,229 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
     (void)hipEventDestroy(f1);
     if (rc == BURG_OK && st && st->unconverged_steps > 0)
         return fail(BURG_ENOCONV, "%d steps hit the pass cap", st->unconverged_steps);
+    return rc;
+}
+
+// LSPG PROM (C/hypernet2D.py:133-200 + gauss_newton_LSPG :1859-1929), lspg.hip.
+// Device-resident: basis in (npod, 2n) planes and their transposes, state w
+// and its transpose, y; the host sees only the residual norm per iteration
+// (the reference's stopping tests) and the kept snapshots.
+int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const double *basis,
+              int max_its, double relnorm_cutoff, double min_delta, double *snaps,
+              int64_t ld_snaps, double *red_coords, int64_t ld_red, int32_t *step_its,
+              double *step_rel, double *times_ms, burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (st) std::memset(st, 0, sizeof *st);
+    if (times_ms) times_ms[0] = times_ms[1] = times_ms[2] = 0.0;
+    if (!w0 || !basis) return fail(BURG_EINVAL, "null w0 or basis");
+    if (c->world > 1) return fail(BURG_EINVAL, "burg_lspg: single-GPU contexts only");
+    if (c->nx != c->ny_total)
+        return fail(BURG_ESHAPE, "burg_lspg: the LSPG Jacobian (row-only JDyec permutation, "
+                                 "C/hypernet2D.py:165-167) needs nx == ny");
+    if (n_pod < 1 || n_pod > kLspgMaxPod)
+        return fail(BURG_EINVAL, "n_pod=%d outside [1, %d]", n_pod, kLspgMaxPod);
+    if (num_steps < 0 || max_its < 1) return fail(BURG_EINVAL, "num_steps < 0 or max_its < 1");
+    if (snaps && ld_snaps < num_steps + 1) return fail(BURG_EINVAL, "ld_snaps < num_steps + 1");
+    if (red_coords && ld_red < num_steps + 1) return fail(BURG_EINVAL, "ld_red < num_steps + 1");
+    if (int e = ensure_scratch(c)) return e;
+    const size_t m = c->m(), n = c->n();
+    const int N = c->nx;
+    const int P = lspg_cols(n_pod);
+    double *d_b = nullptr, *d_bt = nullptr, *d_btT = nullptr, *d_w = nullptr, *d_wT = nullptr,
+           *d_wp = nullptr, *d_y = nullptr, *d_part = nullptr, *d_G = nullptr, *d_chunk = nullptr,
+           *d_tr = nullptr;
+    unsigned *d_err = nullptr;
+    bool registered = false;
+    std::vector<hipEvent_t> evs;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(c->stream);
+        if (registered) (void)hipHostUnregister(snaps);
+        for (auto e : evs) (void)hipEventDestroy(e);
+        dfree(d_b), dfree(d_bt), dfree(d_btT), dfree(d_w), dfree(d_wT), dfree(d_wp), dfree(d_y);
+        dfree(d_part), dfree(d_G), dfree(d_err), dfree(d_chunk), dfree(d_tr);
+    };
+    int rc = BURG_OK;
+#define LCHK(expr)                  \
+    do {                            \
+        if ((rc = (expr)) != 0) {   \
+            cleanup();              \
+            return rc;              \
+        }                           \
+    } while (0)
+#define LHIP(expr)                                                                     \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) {                                                        \
+            rc = fail(BURG_EHIP, "burg_lspg: %s: %s", #expr, hipGetErrorString(e_));   \
+            cleanup();                                                                 \
+            return rc;                                                                 \
+        }                                                                              \
+    } while (0)
+#define LLAUNCH(expr)                                                                  \
+    do {                                                                               \
+        if ((expr) != 0) {                                                             \
+            rc = fail(BURG_EHIP, "burg_lspg: launch %s: %s", #expr,                    \
+                      hipGetErrorString(hipGetLastError()));                           \
+            cleanup();                                                                 \
+            return rc;                                                                 \
+        }                                                                              \
+    } while (0)
+    LCHK(dalloc(&d_b, m * n_pod));
+    LCHK(dalloc(&d_bt, m * n_pod));
+    LHIP(hipMemcpyAsync(d_b, basis, sizeof(double) * m * n_pod, hipMemcpyHostToDevice, c->stream));
+    LLAUNCH(launch_basis_transpose(d_b, d_bt, m, n_pod, c->stream));
+    LHIP(hipStreamSynchronize(c->stream));
+    dfree(d_b);
+    LCHK(dalloc(&d_btT, m * n_pod));
+    for (int p = 0; p < 2 * n_pod; ++p)
+        LLAUNCH(launch_basis_transpose(d_bt + (size_t)p * n, d_btT + (size_t)p * n, N, N,
+                                       c->stream));
+    LCHK(dalloc(&d_w, m));
+    LCHK(dalloc(&d_wT, m));
+    LCHK(dalloc(&d_wp, m));
+    LCHK(dalloc(&d_y, (size_t)kLspgMaxPod + 1));
+    LCHK(dalloc(&d_part, lspg_partial_count(N, n_pod)));
+    LCHK(dalloc(&d_G, (size_t)P * P));
+    LCHK(dalloc(&d_err, 1));
+    LHIP(hipMemsetAsync(d_err, 0, sizeof(unsigned), c->stream));
+
+    // kept snapshots: S states at a time, transposed into the C-order columns
+    int S = 0;
+    std::vector<const double *> slots;
+    int64_t col0 = 0;
+    float flush_ms = 0.f;
+    if (snaps) {
+        size_t freeb = 0, totalb = 0;
+        LHIP(hipMemGetInfo(&freeb, &totalb));
+        S = (int)std::min<int64_t>(num_steps + 1, 64);
+        while (S > 1 && (size_t)S * 2 * m * sizeof(double) > freeb / 4) S /= 2;
+        LCHK(dalloc(&d_chunk, (size_t)S * m));
+        LCHK(dalloc(&d_tr, (size_t)S * m));
+        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
+                                     hipHostRegisterDefault) == hipSuccess;
+        (void)hipGetLastError();
+    }
+    std::vector<double> yh((size_t)n_pod);
+    for (int k = 0; k < 8; ++k) {
+        hipEvent_t e = nullptr;
+        LHIP(hipEventCreate(&e));
+        evs.push_back(e);
+    }
+    float t_jac = 0.f, t_res = 0.f, t_ls = 0.f;
+    auto elapsed = [&](int a, int b) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, evs[a], evs[b]);
+        return t;
+    };
+    auto flush = [&]() -> int {
+        if (slots.empty()) return 0;
+        HIPCHK(hipEventRecord(evs[6], c->stream));
+        CHK(launch_transpose(slots.data(), (int)slots.size(), m, d_tr, (int)slots.size(),
+                             c->stream));
+        HIPCHK(hipMemcpy2DAsync(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
+                                slots.size() * sizeof(double), slots.size() * sizeof(double), m,
+                                hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipEventRecord(evs[7], c->stream));
+        HIPCHK(hipEventSynchronize(evs[7]));
+        flush_ms += elapsed(6, 7);
+        col0 += (int64_t)slots.size();
+        slots.clear();
+        return 0;
+    };
+    // keep column j: w -> snapshot slot, y -> red_coords[:, j]
+    auto keep = [&](int64_t j) -> int {
+        if (snaps) {
+            double *slot = d_chunk + slots.size() * m;
+            HIPCHK(hipMemcpyAsync(slot, d_w, m * sizeof(double), hipMemcpyDeviceToDevice,
+                                  c->stream));
+            slots.push_back(slot);
+            if ((int)slots.size() == S)
+                if (int e = flush()) return e;
+        }
+        if (red_coords) {
+            HIPCHK(hipMemcpyAsync(yh.data(), d_y, sizeof(double) * n_pod, hipMemcpyDeviceToHost,
+                                  c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            for (int k = 0; k < n_pod; ++k) red_coords[(size_t)k * ld_red + j] = yh[k];
+        }
+        return 0;
+    };
+    auto expand = [&]() -> int {  // w = basis y and its transposed planes
+        CHK(launch_lspg_expand(d_bt, d_y, n_pod, m, d_w, c->stream));
+        CHK(launch_basis_transpose(d_w, d_wT, N, N, c->stream));
+        CHK(launch_basis_transpose(d_w + n, d_wT + n, N, N, c->stream));
+        return 0;
+    };
+    auto resnorm = [&](double *out) -> int {
+        HIPCHK(hipEventRecord(evs[2], c->stream));
+        if (int e = residual_norm(c, d_w, d_wp, c->d_r, out)) return e;
+        HIPCHK(hipEventRecord(evs[3], c->stream));
+        HIPCHK(hipEventSynchronize(evs[3]));
+        t_res += elapsed(2, 3);
+        return 0;
+    };
+
+    const auto t0 = std::chrono::steady_clock::now();
+    LHIP(hipMemcpyAsync(d_wp, w0, m * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    LLAUNCH(launch_lspg_project(d_bt, d_wp, n_pod, m, d_part, d_y, c->stream));  // y0 = V^T w0
+    LCHK(expand());                                                              // w0 = V y0
+    LCHK(keep(0));
+    LspgArgs la{c->cf, d_w, d_wT, d_bt, d_btT, c->d_r, n_pod};
+    int64_t total_its = 0;
+    for (int s = 0; s < num_steps; ++s) {
+        LHIP(hipMemcpyAsync(d_wp, d_w, m * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        double init = 0.0, rn = 0.0, prev = 0.0;
+        LCHK(resnorm(&init));
+        if (!std::isfinite(init)) {
+            rc = fail(BURG_ENAN, "non-finite residual norm at LSPG step %d", s);
+            break;
+        }
+        int nres = 0;
+        for (int i = 0; i < max_its; ++i) {
+            if (i > 0) LCHK(resnorm(&rn));
+            else rn = init;  // func(w) at the same w as init_norm (:1898-1902)
+            ++nres;
+            if (rn / init < relnorm_cutoff) break;
+            if (nres > 1 && std::fabs((prev - rn) / prev) < min_delta) break;
+            prev = rn;
+            LHIP(hipEventRecord(evs[0], c->stream));
+            LLAUNCH(launch_lspg_gram(la, d_part, d_G, c->stream));
+            LHIP(hipEventRecord(evs[1], c->stream));
+            LLAUNCH(launch_lspg_solve(d_G, n_pod, d_y, nullptr, d_err, c->stream));
+            LCHK(expand());
+            LHIP(hipEventRecord(evs[4], c->stream));
+            LHIP(hipEventSynchronize(evs[4]));
+            t_jac += elapsed(0, 1);
+            t_ls += elapsed(1, 4);
+            ++total_its;
+        }
+        unsigned err = 0;
+        LHIP(hipMemcpy(&err, d_err, sizeof err, hipMemcpyDeviceToHost));
+        if (err) {
+            rc = fail(BURG_ENOCONV, "LSPG step %d: J basis is rank-deficient (Cholesky pivot <= 0)", s);
+            break;
+        }
+        if (step_its) step_its[s] = nres;
+        if (step_rel) step_rel[s] = rn / init;
+        if (st) st->last_rel = rn / init;
+        LCHK(keep(s + 1));
+    }
+    if (rc == BURG_OK) LCHK(flush());
+    LHIP(hipStreamSynchronize(c->stream));
+    const double loop_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (st) {
+        st->steps = num_steps;
+        st->newton_updates = total_its;
+        st->loop_ms = loop_ms;
+        st->flush_ms = flush_ms;
+    }
+    if (times_ms) times_ms[0] = t_jac, times_ms[1] = t_res, times_ms[2] = t_ls;
+#undef LCHK
+#undef LHIP
+#undef LLAUNCH
+    cleanup();
     return rc;
 }
 

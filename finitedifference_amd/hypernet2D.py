@@ -208,6 +208,35 @@ def compute_ECSW_training_matrix_2D(snaps, prev_snaps, basis, res=None, jac=None
     return ctx.ecsw_matrix(snaps, prev_snaps, basis)
 
 
+def inviscid_burgers_implicit2D_LSPG(grid_x, grid_y, w0, dt, num_steps, mu, basis, *, device=0,
+                                     max_its=20, relnorm_cutoff=1e-5, min_delta=0.1,
+                                     verbose=True, return_coords=False):
+    """LSPG PROM time loop (C/hypernet2D.py:133-200) with its Gauss-Newton
+    solver (gauss_newton_LSPG, :1859-1929; max_its / relnorm_cutoff /
+    min_delta are its defaults), on the GPU (burg_lspg).  Same call and
+    result: (snaps (2n, T+1), (num_its, jac_time, res_time, ls_time)), snaps
+    column j = basis @ y_j.  The LSPG Jacobian keeps the reference's row-only
+    JDyec permutation (:165-167; its y-derivative reads the transposed field,
+    lspg.hip), so nx == ny is required, as in the reference.  Each
+    Gauss-Newton update solves the least-squares problem by the normal
+    equations of J.basis (Cholesky) where the reference calls
+    np.linalg.lstsq; the two agree to round-off for a full-rank J.basis.
+    jac_time is the fused J.basis + Gram kernel, res_time the residual
+    kernel, ls_time the solve and the basis expansion (seconds, HIP events).
+    return_coords=True appends the reduced coordinates (npod, T+1)."""
+    if verbose:
+        print(f"Running ROM of size {np.shape(basis)[1]} for mu1={mu[0]}, mu2={mu[1]}")
+    ctx = _ctx_for(grid_x, grid_y, dt, mu, device)
+    snaps, red, its, rel, times, _ = ctx.lspg(w0, num_steps, basis, max_its=max_its,
+                                             relnorm_cutoff=relnorm_cutoff, min_delta=min_delta)
+    if verbose:
+        for i in range(int(num_steps)):
+            print(f" ... Working on timestep {i}")
+            print("iteration {}: relative norm {:3.2e}".format(int(its[i]) - 1, rel[i]))
+    out = (snaps, (int(its.sum()), times[0] / 1e3, times[1] / 1e3, times[2] / 1e3))
+    return out + (red,) if return_coords else out
+
+
 def compute_error(rom_snaps, hdm_snaps):
     """Relative error at each time step (C/hypernet2D.py:3074-3079)."""
     sq_hdm = np.sqrt(np.square(rom_snaps).sum(axis=0))

@@ -212,6 +212,33 @@ class FOMContext:
                                             _lib.dptr(basis), _lib.dptr(C), ctypes.byref(st)))
         return (C, st.as_dict()) if return_stats else C
 
+    def lspg(self, w0, num_steps, basis, max_its=20, relnorm_cutoff=1e-5, min_delta=0.1,
+             keep_snaps=True, keep_coords=True):
+        """LSPG PROM trajectory (burg_lspg; inviscid_burgers_implicit2D_LSPG,
+        C/hypernet2D.py:133-200, gauss_newton_LSPG :1859-1929) on the problem of
+        the last set_problem.  Returns (snaps (2n, T+1) or None, red_coords
+        (npod, T+1) or None, its per step, rel per step, times_ms [jac, res,
+        ls], stats)."""
+        basis = np.ascontiguousarray(np.asarray(basis, dtype=np.float64))
+        if basis.ndim != 2 or basis.shape[0] != self.m:
+            raise ValueError("basis must be (2*nx*ny, n_pod)")
+        w0 = np.ascontiguousarray(np.asarray(w0, dtype=np.float64).ravel())
+        if w0.size != self.m:
+            raise ValueError("w0 must have 2*nx*ny entries")
+        T, npod = int(num_steps), basis.shape[1]
+        snaps = np.zeros((self.m, T + 1)) if keep_snaps else None
+        red = np.zeros((npod, T + 1)) if keep_coords else None
+        its = np.zeros(T, dtype=np.int32)
+        rel = np.zeros(T)
+        times = np.zeros(3)
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_lspg(self._h, _lib.dptr(w0), T, npod, _lib.dptr(basis),
+                                     int(max_its), float(relnorm_cutoff), float(min_delta),
+                                     _lib.dptr(snaps), T + 1, _lib.dptr(red), T + 1,
+                                     _lib.iptr(its), _lib.dptr(rel), _lib.dptr(times),
+                                     ctypes.byref(st)))
+        return snaps, red, its, rel, times, st.as_dict()
+
     def kernel_bench(self, kernel="residual", reps=20):
         """Mean device time (ms) of one launch of the residual or J.x stencil
         on device-resident operands (burg_kernel_bench; upload() first)."""

@@ -18,6 +18,8 @@
  *   burg_sweep          a loop of inviscid_burgers_implicit2D over a mu set
  *                       (C/run_prom.py:59-71, C/run_tests.py:38-49)
  *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
+ *   burg_lspg           C/hypernet2D.py:133-200   inviscid_burgers_implicit2D_LSPG
+ *                       with C/hypernet2D.py:1859-1929 gauss_newton_LSPG
  *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
  *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
  *
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 4
+#define BURG_ABI_VERSION 5
 
 enum burg_status {
     BURG_OK = 0,
@@ -222,6 +224,30 @@ int burg_sweep(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b,
  * D2H time of C, steps = n_snaps.  Single-GPU contexts. */
 int burg_ecsw_matrix(burg_ctx *ctx, int n_snaps, const double *states, const double *prev_states,
                      int n_pod, const double *basis, double *C, burg_stats *stats);
+
+/* LSPG PROM time loop (inviscid_burgers_implicit2D_LSPG, C/hypernet2D.py:133-200,
+ * with gauss_newton_LSPG, :1859-1929), with the context's problem (grid, dt,
+ * mu of burg_set_problem); square single-GPU contexts (the reference's
+ * row-only JDyec permutation, :165-167, is defined for nx == ny only).
+ *   y0 = basis^T w0, w = basis y0; per step: Gauss-Newton from the previous
+ *   y, stopping at ||R||/||R(w at entry)|| < relnorm_cutoff, or when the
+ *   relative change of ||R|| is below min_delta, or after max_its norms;
+ *   each update solves min ||J(w) basis dy + R|| (normal equations,
+ *   Cholesky; the reference: np.linalg.lstsq).
+ * basis: (2n x n_pod) C-order, 1 <= n_pod <= 127.  snaps (NULL: not kept):
+ * (2n x ld_snaps) C-order, column j = basis y_j (j = 0..num_steps);
+ * red_coords (NULL: not kept): (n_pod x ld_red) C-order, column j = y_j;
+ * step_its (NULL ok): per step, len(resnorms) of the reference (its printed
+ * 'iteration i' + 1); step_rel (NULL ok): the printed relative norm.
+ * times_ms (NULL ok): [0] fused J.basis + Gram kernel time, [1] residual
+ * time, [2] solve + basis expansion time (HIP events; the reference's
+ * jac_time, res_time, ls_time).  stats: steps, newton_updates = total
+ * Gauss-Newton updates, loop_ms = wall time, flush_ms = snapshot D2H.
+ * Returns BURG_ENOCONV when J basis is rank-deficient (Cholesky pivot <= 0). */
+int burg_lspg(burg_ctx *ctx, const double *w0, int num_steps, int n_pod, const double *basis,
+              int max_its, double relnorm_cutoff, double min_delta, double *snaps,
+              int64_t ld_snaps, double *red_coords, int64_t ld_red, int32_t *step_its,
+              double *step_rel, double *times_ms, burg_stats *stats);
 
 #ifdef __cplusplus
 }

@@ -146,6 +146,70 @@ class Problem:
             C[i * npod:(i + 1) * npod, :] = (r[:n, None] * Wi[:n] + r[n:, None] * Wi[n:]).T
         return C
 
+    def lspg_jvp(self, w, x):
+        """J_LSPG(w) @ x of inviscid_burgers_implicit2D_LSPG (C/hypernet2D.py:133-200):
+        exact_jac2D (:2627-2656) with the driver's JDyec = kron(I, Dy)[perm, :]
+        (rows permuted only, :165-167; the FOM permutes rows and columns,
+        :98-106).  For nx == ny that operator is (Y f)[r, c] =
+        f[c, r]/dy_r - f[c, r-1]/dy_{r-1}: the y-difference of the transposed
+        field.  JDxec = kron(I, Dx) is the row-wise backward difference
+        (make_ddx, :2410-2416)."""
+        assert self.nx == self.ny, "the LSPG Jacobian is defined for square grids"
+        N, n, a = self.nx, self.nx * self.nx, 0.5 * self.dt
+        u, v = w[:n].reshape(N, N), w[n:].reshape(N, N)
+        xu, xv = x[:n].reshape(N, N), x[n:].reshape(N, N)
+
+        def Dx(f):
+            g = f * self.inv_dx[None, :]
+            out = g.copy()
+            out[:, 1:] -= g[:, :-1]
+            return out
+
+        def Y(f):
+            g = f.T * self.inv_dy[:, None]
+            out = g.copy()
+            out[1:, :] -= g[:-1, :]
+            return out
+
+        yu = xu + Dx(a * u * xu) + 0.5 * Y(a * v * xu) + 0.5 * Y(a * u * xv)
+        yv = xv + 0.5 * Dx(a * v * xu) + Y(a * v * xv) + 0.5 * Dx(a * u * xv)
+        return np.concatenate((yu.ravel(), yv.ravel()))
+
+    def lspg(self, w0, num_steps, basis, max_its=20, relnorm_cutoff=1e-5, min_delta=0.1):
+        """inviscid_burgers_implicit2D_LSPG (C/hypernet2D.py:133-200) with
+        gauss_newton_LSPG (:1859-1929) restated: y0 = basis^T w0; per step
+        Gauss-Newton from the previous y with np.linalg.lstsq(J basis, -R).
+        The residual is orc_residual (res2D_alt op order; the reference's LSPG
+        calls res2D, equal to round-off).  Returns (snaps (2n, T+1), its per
+        step = len(resnorms), rel per step = the printed relative norm)."""
+        basis = np.asarray(basis, dtype=np.float64)
+        npod = basis.shape[1]
+        y = basis.T.dot(w0)
+        w = basis.dot(y)
+        snaps = np.zeros((self.m, num_steps + 1))
+        snaps[:, 0] = w
+        its = np.zeros(num_steps, dtype=np.int32)
+        rels = np.zeros(num_steps)
+        for s in range(num_steps):
+            wp = w.copy()
+            init = np.linalg.norm(self.residual(w, wp))
+            resnorms = []
+            for i in range(max_its):
+                f = self.residual(w, wp)
+                rn = np.linalg.norm(f)
+                resnorms.append(rn)
+                if rn / init < relnorm_cutoff:
+                    break
+                if len(resnorms) > 1 and abs((resnorms[-2] - resnorms[-1]) / resnorms[-2]) < min_delta:
+                    break
+                JV = np.stack([self.lspg_jvp(w, basis[:, k]) for k in range(npod)], axis=1)
+                dy = np.linalg.lstsq(JV, -f, rcond=None)[0]
+                y = y + dy
+                w = basis.dot(y)
+            its[s], rels[s] = len(resnorms), rn / init
+            snaps[:, s + 1] = w
+        return snaps, its, rels
+
 
 def rel_l2(a, b):
     a, b = np.asarray(a), np.asarray(b)

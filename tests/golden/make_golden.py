@@ -27,6 +27,12 @@ Fixtures written
                      reference's own callbacks (res2D, exact_jac2D) on
                      reference snapshots, the driver's 3-step offset sampling
                      (C/run_HPROM_ecsw_joshua_.py:81-84) and a POD basis
+  ref_lspg.npz       inviscid_burgers_implicit2D_LSPG (:133-200) + gauss_newton_LSPG
+                     (:1859-1929) trajectories with POD bases of reference
+                     snapshots at training mu, per-step Gauss-Newton counts
+                     (from its printed 'iteration i' lines), and the LSPG
+                     Jacobian (row-only JDyec permutation, :165-167) times the
+                     basis at a random state
   author_logs.json   Newton counts/residuals from the author's SLURM log
                      F/output_55034725.log (750^2)
 """
@@ -152,6 +158,44 @@ def make_ecsw(hn):
     np.savez_compressed(os.path.join(HERE, "ref_ecsw.npz"), **out)
 
 
+GN_RE = re.compile(r"^iteration (\d+): relative norm ([0-9.eE+-]+)\s*$")
+
+
+def make_lspg(hn):
+    import scipy.sparse as sp
+    rng = np.random.default_rng(SEED)
+    out = {}
+    # (tag, N, T, training mus, npod, rom mu)
+    for tag, N, T, train, npod, mu in (
+            ("n16", 16, 30, ((4.25, 0.015), (5.5, 0.03)), 6, (4.75, 0.02)),
+            ("n24", 24, 20, ((4.25, 0.015), (5.5, 0.03), (5.19, 0.026)), 12, (4.56, 0.019)),
+            ("n32", 32, 12, ((4.25, 0.03), (5.5, 0.015)), 20, (5.19, 0.026))):
+        gx, gy = hn.make_2D_grid(0, 100, 0, 100, N, N)
+        S = np.hstack([run_reference(hn, N, T, m)[0] for m in train])
+        basis = np.linalg.svd(S, full_matrices=False)[0][:, :npod]
+        w0 = np.ones(2 * N * N)
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            snaps, stats = hn.inviscid_burgers_implicit2D_LSPG(gx, gy, w0, 0.05, T, list(mu), basis)
+        gn = [GN_RE.match(l.strip()) for l in buf.getvalue().splitlines()]
+        its = np.array([int(m.group(1)) + 1 for m in gn if m], dtype=np.int32)
+        rel = np.array([float(m.group(2)) for m in gn if m])
+        assert its.size == T and its.sum() == stats[0], (its, stats)
+        # the LSPG Jacobian (JDyec rows permuted only, :165-167) times the basis
+        Dxec, Dyec = hn.make_ddx(gx), hn.make_ddx(gy)
+        JDxec = sp.kron(sp.eye(N), Dxec)
+        JDyec = sp.kron(sp.eye(N), Dyec)
+        JDyec = JDyec.tocsr()[np.arange(N * N).reshape(N, -1).T.flatten(), :]
+        Eye = sp.eye(2 * N * N)
+        w = rng.uniform(1.0, 6.0, 2 * N * N)
+        JV = hn.inviscid_burgers_exact_jac2D(w, 0.05, JDxec, JDyec, Eye).dot(basis)
+        out.update({f"{tag}_snaps": snaps, f"{tag}_basis": basis, f"{tag}_its": its,
+                    f"{tag}_rel": rel, f"{tag}_w": w, f"{tag}_JV": JV,
+                    f"{tag}_meta": np.array([N, T, mu[0], mu[1], 0.05, npod])})
+        print(f"lspg {tag}: its {its.tolist()}")
+    np.savez_compressed(os.path.join(HERE, "ref_lspg.npz"), **out)
+
+
 def _summaries(snaps, N, steps_full):
     n = N * N
     T1 = snaps.shape[1]
@@ -275,6 +319,8 @@ def main():
             make_ops(hn)
         if not only or "ecsw" in only:
             make_ecsw(hn)
+        if not only or "lspg" in only:
+            make_lspg(hn)
         if not only or "coarse" in only:
             make_coarse250(hn, args.coarse_npy, args.coarse_log)
         if (not only or "fine" in only) and not args.skip_750:

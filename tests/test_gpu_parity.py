@@ -506,3 +506,59 @@ def test_ecsw_matrix_multiblock_bitwise(gpu, orc):
     C, st = ctx.ecsw_matrix(snaps, prev, basis, return_stats=True)
     assert C.shape == (npod * ns, N * N) and st["steps"] == ns
     assert np.array_equal(C, P.ecsw_matrix(snaps, prev, basis))
+
+
+# ------------------------------------------------ LSPG PROM --
+@pytest.mark.parametrize("tag", ["n16", "n24", "n32"])
+def test_lspg_vs_reference_and_oracle(gpu, orc, tag):
+    """inviscid_burgers_implicit2D_LSPG on the GPU (burg_lspg: fused J.basis +
+    Gram kernel, Cholesky of the normal equations) against the reference's own
+    ROM trajectory (tests/golden/ref_lspg.npz: POD bases of reference
+    snapshots, out-of-sample mu) and the oracle restatement (lstsq).  Bars:
+    same Gauss-Newton count every step; trajectory within 1e-10 rel-L2 (the
+    north-star fp64 bar); reduced coordinates consistent with the snapshots."""
+    from finitedifference_amd import hypernet2D as H
+    g = golden("ref_lspg.npz")
+    N, T, m1, m2, dt, npod = g[f"{tag}_meta"]
+    N, T, npod = int(N), int(T), int(npod)
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    B = g[f"{tag}_basis"]
+    snaps, (nits, tj, tr, tl), red = H.inviscid_burgers_implicit2D_LSPG(
+        gx, gy, np.ones(2 * N * N), dt, T, (m1, m2), B, verbose=False, return_coords=True)
+    assert snaps.shape == (2 * N * N, T + 1) and red.shape == (npod, T + 1)
+    assert nits == int(g[f"{tag}_its"].sum())
+    assert rel(snaps, g[f"{tag}_snaps"]) <= REF_TOL
+    P = orc.Problem(N, dt=dt, mu=(m1, m2))
+    osnaps, oits, _ = P.lspg(np.ones(2 * N * N), T, B)
+    assert np.array_equal(oits, g[f"{tag}_its"])
+    assert rel(snaps, osnaps) <= REF_TOL
+    assert rel(B @ red, snaps) <= 1e-14
+    assert min(tj, tr, tl) >= 0.0
+
+
+def test_lspg_step_counts_and_rank_errors(gpu, orc):
+    """Per-step counts/relative norms through the context API; a ragged grid
+    (N not a multiple of the 16-cell tile), npod at the 127 cap, and the
+    errors the boundary promises (non-square grid, npod out of range,
+    rank-deficient basis)."""
+    from finitedifference_amd import _lib
+    N, T = 37, 4
+    P = orc.Problem(N, mu=(4.9, 0.021))
+    sn, _, _ = P.fom(np.ones(P.m), 12, solver="march")
+    S = sn.T
+    rng = np.random.default_rng(7)
+    B = np.linalg.qr(np.hstack([S, rng.standard_normal((P.m, 127 - S.shape[1]))]))[0]
+    ctx = make_ctx(N, mu=(4.9, 0.021))
+    snaps, red, its, rels, times, st = ctx.lspg(np.ones(P.m), T, B)
+    osnaps, oits, orels = P.lspg(np.ones(P.m), T, B)
+    assert np.array_equal(its, oits)
+    assert int((its - 1).sum()) <= st["newton_updates"] <= int(its.sum())
+    assert rel(snaps, osnaps) <= REF_TOL
+    assert np.allclose(rels, orels, rtol=1e-6, atol=1e-12)
+    with pytest.raises(_lib.BurgersError):
+        ctx.lspg(np.ones(P.m), 1, np.zeros((P.m, 128)))
+    with pytest.raises(_lib.BurgersError):  # J basis rank-deficient: two equal columns
+        ctx.lspg(np.ones(P.m), 1, np.hstack([B[:, :3], B[:, :1]]))
+    sq = make_ctx(N, ny=N + 3)
+    with pytest.raises(_lib.BurgersError):
+        sq.lspg(np.ones(2 * N * (N + 3)), 1, np.ones((2 * N * (N + 3), 2)))

@@ -199,3 +199,25 @@ def test_oracle_ecsw_matrix_vs_reference():
         ref = g[f"{tag}_C"]
         assert C.shape == ref.shape == (int(npod) * len(range(3, T, f)), N * N)
         assert np.linalg.norm(C - ref) <= 1e-14 * np.linalg.norm(ref)
+
+
+# ------------------------------------------------ LSPG PROM --
+@pytest.mark.parametrize("tag", ["n16", "n24", "n32"])
+def test_oracle_lspg_vs_reference(orc, tag):
+    """oracle Problem.lspg_jvp / lspg (restating inviscid_burgers_implicit2D_LSPG,
+    C/hypernet2D.py:133-200, and gauss_newton_LSPG, :1859-1929) against the
+    reference's own outputs (tests/golden/ref_lspg.npz): the LSPG Jacobian with
+    the row-only JDyec permutation times the basis, the ROM trajectory and the
+    per-step Gauss-Newton counts (its printed 'iteration i' lines; the printed
+    relative norm carries 3 significant digits)."""
+    g = golden("ref_lspg.npz")
+    N, T, m1, m2, dt, npod = g[f"{tag}_meta"]
+    N, T, npod = int(N), int(T), int(npod)
+    P = orc.Problem(N, dt=dt, mu=(m1, m2))
+    B = g[f"{tag}_basis"]
+    JV = np.stack([P.lspg_jvp(g[f"{tag}_w"], B[:, k]) for k in range(npod)], axis=1)
+    assert orc.rel_l2(JV, g[f"{tag}_JV"]) < 1e-14
+    snaps, its, rels = P.lspg(np.ones(2 * N * N), T, B)
+    assert orc.rel_l2(snaps, g[f"{tag}_snaps"]) < 1e-13
+    assert np.array_equal(its, g[f"{tag}_its"])
+    assert np.allclose(rels, g[f"{tag}_rel"], rtol=1e-2)
