@@ -73,16 +73,26 @@ __global__ __launch_bounds__(kLB) void lspg_project_kernel(const double *__restr
     if (threadIdx.x == 0) partial[(size_t)k * nb + blockIdx.x] = red[0];
 }
 
-// out[e] = sum_g partial[g * stride + e] (fixed order: deterministic)
+// out[y * ne + e] = sum over groups g in slice y (= blockIdx.y of gridDim.y) of
+// partial[g * stride + e]; fixed order, deterministic
 __global__ __launch_bounds__(kLB) void lspg_sum_kernel(const double *__restrict__ partial,
                                                        int ng, size_t stride, int ne,
                                                        double *__restrict__ out)
 {
     const int e = blockIdx.x * kLB + threadIdx.x;
     if (e >= ne) return;
-    double s = 0.0;
-    for (int g = 0; g < ng; ++g) s += partial[(size_t)g * stride + e];
-    out[e] = s;
+    const int ns = gridDim.y, y = blockIdx.y;
+    const int g0 = (int)((long long)ng * y / ns), g1 = (int)((long long)ng * (y + 1) / ns);
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int g = g0;
+    for (; g + 3 < g1; g += 4) {
+        s0 += partial[(size_t)g * stride + e];
+        s1 += partial[(size_t)(g + 1) * stride + e];
+        s2 += partial[(size_t)(g + 2) * stride + e];
+        s3 += partial[(size_t)(g + 3) * stride + e];
+    }
+    for (; g < g1; ++g) s0 += partial[(size_t)g * stride + e];
+    out[(size_t)y * ne + e] = (s0 + s1) + (s2 + s3);
 }
 
 // per-k partial layout of the projection: out[k] = sum_b partial[k nb + b]
@@ -182,70 +192,210 @@ __global__ __launch_bounds__(kLB) void lspg_gram_kernel(LspgArgs a, double *__re
         for (int q = 0; q < TB; ++q) out[(bi * TB + p) * P + bj * TB + q] = acc[p][q];
 }
 
-// One workgroup: Cholesky of G[0:npod, 0:npod] (ld P), forward and back
-// substitution against b = G[0:npod, npod], then y += dy.  err <- 1 when a
+// Fused JV + augmented Gram on the matrix cores (v_mfma_f64_16x16x4_f64).
+// A tile = kMC consecutive cells = 2 kMC rows of X = [JV | -R] staged in LDS
+// (u-rows 0..kMC-1, v-rows kMC..2kMC-1; filled with lane = cell, so every
+// basis-plane load is a contiguous run of cells).  G = X^T X is symmetric:
+// only the NB (NB + 1) / 2 upper 16 x 16 blocks are formed, block pair p owned
+// by wave p % 4 for the whole launch (no cross-wave reduction).  Per 4-row
+// step a lane feeds A = X[row 4s + (l >> 4)][16 b1 + (l & 15)] and the same
+// for b2 (the f64 16x16x4 operand map: A[m = l & 15][k = l >> 4],
+// B[k = l >> 4][n = l & 15]); D lane l register i = G[16 b1 + (l >> 4) + 4 i]
+// [16 b2 + (l & 15)] (cdna_hip_programming.md, f64 MFMA layout).  The row
+// stride LD = P + 17 doubles keeps both the fill stores (lane = row) and the
+// operand reads (4 rows x 16 columns) free of LDS bank conflicts.
+constexpr int kMC = 32;
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+template <int NB>
+__global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double *__restrict__ partial)
+{
+    constexpr int P = 16 * NB;
+    constexpr int LD = P + 17;
+    constexpr int NPAIR = NB * (NB + 1) / 2;
+    constexpr int NQ = (NPAIR + 3) / 4;
+    __shared__ double X[2 * kMC * LD];
+    const int N = a.cf.nx;
+    const size_t n = (size_t)N * N, m = 2 * n;
+    const double al = a.cf.alpha;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    // this wave's block pairs (upper triangle, row-major enumeration)
+    int pb1[NQ], pb2[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        int p = wv + 4 * q, b1 = 0;
+        if (p >= NPAIR) p = -1;
+        int rem = p;
+        while (rem >= 0 && rem >= NB - b1) {
+            rem -= NB - b1;
+            ++b1;
+        }
+        pb1[q] = p < 0 ? -1 : b1;
+        pb2[q] = p < 0 ? -1 : b1 + rem;
+    }
+    dbl4 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+
+    const int j = tid & (kMC - 1), kg = tid / kMC;  // fill role: cell j, columns kg + 8 q
+    const int orow = lane >> 4, ocol = lane & 15;    // MFMA operand role
+    const size_t ntiles = (n + kMC - 1) / kMC;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const size_t i = t * kMC + j;
+        const bool ok = i < n;
+        const size_t ii = ok ? i : n - 1;
+        const int r = (int)(ii / N), c = (int)(ii - (size_t)r * N);
+        const bool west = c > 0, south = r > 0;
+        const size_t iw = west ? ii - 1 : ii, is = south ? ii - N : ii;
+        const double *u = a.w, *v = a.w + n, *uT = a.wT, *vT = a.wT + n;
+        const double ui = u[ii], vi = v[ii], uW = u[iw], vW = v[iw];
+        const double uTi = uT[ii], vTi = vT[ii], uTS = uT[is], vTS = vT[is];
+        const double ax = al * a.cf.inv_dx[c], axw = west ? al * a.cf.inv_dx[c - 1] : 0.0;
+        const double ay = al * a.cf.inv_dy[r], ays = south ? al * a.cf.inv_dy[r - 1] : 0.0;
+#pragma unroll 4
+        for (int k = kg; k < P; k += kLB / kMC) {
+            double yu = 0.0, yv = 0.0;
+            if (ok && k < a.npod) {
+                const double *xu = a.bt + (size_t)k * m, *xv = xu + n;
+                const double *xuT = a.btT + (size_t)k * m, *xvT = xuT + n;
+                const double xui = xu[ii], xvi = xv[ii], xuw = xu[iw], xvw = xv[iw];
+                const double xuTi = xuT[ii], xvTi = xvT[ii], xuTS = xuT[is], xvTS = xvT[is];
+                const double mT = vTi * xuTi + uTi * xvTi;
+                yu = xui + ax * (ui * xui) + 0.5 * ay * mT;
+                yv = xvi + ay * (vTi * xvTi) + 0.5 * ax * (vi * xui + ui * xvi);
+                if (west) {
+                    yu -= axw * (uW * xuw);
+                    yv -= 0.5 * axw * (vW * xuw + uW * xvw);
+                }
+                if (south) {
+                    yu -= 0.5 * ays * (vTS * xuTS + uTS * xvTS);
+                    yv -= ays * (vTS * xvTS);
+                }
+            } else if (ok && k == a.npod) {
+                yu = -a.r[ii];
+                yv = -a.r[n + ii];
+            }
+            X[j * LD + k] = yu;
+            X[(kMC + j) * LD + k] = yv;
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int s4 = 0; s4 < 2 * kMC; s4 += 4) {
+            const double *xr = X + (s4 + orow) * LD + ocol;
+#pragma unroll
+            for (int q = 0; q < NQ; ++q) {
+                if (pb1[q] < 0) continue;
+                const double av = xr[16 * pb1[q]], bv = xr[16 * pb2[q]];
+                acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+            }
+        }
+        __syncthreads();
+    }
+    double *out = partial + (size_t)blockIdx.x * P * P;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (pb1[q] < 0) continue;
+        const int r0 = 16 * pb1[q], c0 = 16 * pb2[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rr = r0 + orow + 4 * e, cc = c0 + ocol;
+            out[(size_t)rr * P + cc] = acc[q][e];
+            if (pb1[q] != pb2[q]) out[(size_t)cc * P + rr] = acc[q][e];
+        }
+    }
+}
+
+// LDS row stride of the Cholesky factor: LD = 1 (mod 32) doubles, so a column
+// (lane = row) spreads over all 64 banks and a row (lane = column) too
+__host__ __device__ inline int lspg_solve_ld(int npod) { return npod + ((33 - npod % 32) % 32); }
+
+// One workgroup: Cholesky of the augmented matrix [[G, b], [b^T, .]]
+// (G = G[0:npod, 0:npod], b = G[0:npod, npod], ld P -- the Gram kernel's
+// augmented column), so the factor's last row is L^-1 b and no forward
+// substitution is needed; then L^T dy = L^-1 b and y += dy.  err <- 1 when a
 // pivot is not positive relative to its diagonal (rank-deficient JV).
+// One barrier per column: column jj is consumed unscaled (L_ij L_kj / d) by
+// the trailing update and its scaled copy is written to the unused upper
+// triangle (row jj), where the back substitution reads it.
 __global__ __launch_bounds__(kLB) void lspg_solve_kernel(const double *__restrict__ G, int P,
                                                          int npod, double *__restrict__ y,
                                                          double *__restrict__ dy_out,
                                                          unsigned *__restrict__ err)
 {
-    extern __shared__ double L[];  // npod x (npod + 1), dynamic (up to 127 x 128 doubles)
-    __shared__ double z[kLspgMaxPod], d0[kLspgMaxPod];
+    extern __shared__ double L[];  // (npod + 1) x LD, dynamic (lspg_solve_ld)
+    __shared__ double rdg[kLspgMaxPod], d0[kLspgMaxPod], dyv[kLspgMaxPod];
     __shared__ int bad;
-    const int LD = npod + 1, tid = threadIdx.x;
-    for (int e = tid; e < npod * npod; e += kLB) {
-        const int i = e / npod, k = e - i * npod;
+    const int n1 = npod + 1;
+    const int LD = lspg_solve_ld(n1), tid = threadIdx.x;
+    for (int e = tid; e < n1 * n1; e += kLB) {
+        const int i = e / n1, k = e - i * n1;
         L[i * LD + k] = G[(size_t)i * P + k];
     }
-    for (int i = tid; i < npod; i += kLB) {
-        z[i] = G[(size_t)i * P + npod];
-        d0[i] = G[(size_t)i * P + i];
-    }
+    for (int i = tid; i < npod; i += kLB) d0[i] = G[(size_t)i * P + i];
     if (tid == 0) bad = 0;
     __syncthreads();
+    const int kk = tid & 127, half = tid >> 7;
     for (int jj = 0; jj < npod; ++jj) {
+        const double d = L[jj * LD + jj];
+        const double dd = d > 0.0 ? d : 1.0;
+        const double rp = rsqrt(dd), rd = 1.0 / dd;
         if (tid == 0) {
-            const double d = L[jj * LD + jj];
             // a pivot that lost all but ~8 ulp of its column's norm: rank-deficient
             if (!(d > 0x1p-49 * d0[jj])) bad = 1;
-            L[jj * LD + jj] = sqrt(d > 0.0 ? d : 1.0);
+            rdg[jj] = rp;
         }
-        __syncthreads();
-        const double piv = L[jj * LD + jj];
-        for (int i = jj + 1 + tid; i < npod; i += kLB) L[i * LD + jj] /= piv;
-        __syncthreads();
-        const int rem = npod - jj - 1;
-        for (int e = tid; e < rem * rem; e += kLB) {
-            const int i = jj + 1 + e / rem, k = jj + 1 + e % rem;
-            if (k <= i) L[i * LD + k] -= L[i * LD + jj] * L[k * LD + jj];
+        // scaled column jj (rows jj+1..npod) -> upper row jj
+        for (int i = jj + 1 + tid; i <= npod; i += kLB) L[jj * LD + i] = L[i * LD + jj] * rp;
+        const int k = jj + 1 + kk;
+        if (k <= npod) {
+            // rows i >= k of this half, 8 at a time: all loads issued before
+            // the stores (the rows are distinct; one LDS latency per 8 rows)
+            const double lk = L[k * LD + jj] * rd;
+            const int i00 = k - ((k - (jj + 1 + half)) & 1);
+            for (int i0 = i00; i0 <= npod; i0 += 16) {
+                double li[8], lik[8];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + 2 * q;
+                    const bool on = i <= npod && i >= k;
+                    li[q] = on ? L[i * LD + jj] : 0.0;
+                    lik[q] = on ? L[i * LD + k] : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int i = i0 + 2 * q;
+                    if (i <= npod && i >= k) L[i * LD + k] = lik[q] - li[q] * lk;
+                }
+            }
         }
         __syncthreads();
     }
-    // L z' = b (in place in z), then L^T dy = z'
-    for (int jj = 0; jj < npod; ++jj) {
-        if (tid == 0) z[jj] /= L[jj * LD + jj];
-        __syncthreads();
-        for (int i = jj + 1 + tid; i < npod; i += kLB) z[i] -= L[i * LD + jj] * z[jj];
-        __syncthreads();
-    }
+    // L^T dy = z, z_j = (L^-1 b)_j = upper row j, column npod; L^T row j = upper row j
     for (int jj = npod - 1; jj >= 0; --jj) {
-        if (tid == 0) z[jj] /= L[jj * LD + jj];
-        __syncthreads();
-        for (int i = tid; i < jj; i += kLB) z[i] -= L[jj * LD + i] * z[jj];
+        const double dj = L[jj * LD + npod] * rdg[jj];
+        if (tid == 0) dyv[jj] = dj;
+        for (int i = tid; i < jj; i += kLB) L[i * LD + npod] -= L[i * LD + jj] * dj;
         __syncthreads();
     }
     for (int i = tid; i < npod; i += kLB) {
-        y[i] += z[i];
-        if (dy_out) dy_out[i] = z[i];
+        y[i] += dyv[i];
+        if (dy_out) dy_out[i] = dyv[i];
     }
     if (tid == 0 && bad) *err = 1u;
 }
 
-int groups_for(size_t n)
+constexpr int kMfmaGroups = 512;  // 2 per CU (57 KB of LDS each at P = 96)
+constexpr int kSumSlices = 16;
+
+// the MFMA kernel serves P <= 96 (npod <= 95); P = 128 uses the vector kernel
+bool use_mfma(int P) { return P <= 96; }
+
+int groups_for(size_t n, int P)
 {
-    const size_t tiles = (n + kGC - 1) / kGC;
-    return (int)(tiles < (size_t)kGroups ? tiles : (size_t)kGroups);
+    const size_t cells = use_mfma(P) ? kMC : kGC;
+    const size_t cap = use_mfma(P) ? kMfmaGroups : kGroups;
+    const size_t tiles = (n + cells - 1) / cells;
+    return (int)(tiles < cap ? tiles : cap);
 }
 
 }  // namespace
@@ -260,7 +410,7 @@ int lspg_cols(int npod)
 size_t lspg_partial_count(int nx, int npod)
 {
     const int P = lspg_cols(npod);
-    return (size_t)groups_for((size_t)nx * nx) * P * P + (size_t)npod * 256;
+    return (size_t)(groups_for((size_t)nx * nx, P) + kSumSlices) * P * P + (size_t)npod * 256;
 }
 
 int launch_lspg_expand(const double *bt, const double *y, int npod, size_t m, double *w,
@@ -285,16 +435,21 @@ int launch_lspg_project(const double *bt, const double *x, int npod, size_t m, d
 int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t st)
 {
     const int P = lspg_cols(a.npod);
-    const int ng = groups_for((size_t)a.cf.nx * a.cf.nx);
+    const int ng = groups_for((size_t)a.cf.nx * a.cf.nx, P);
     switch (P) {
-    case 32: hipLaunchKernelGGL(lspg_gram_kernel<2>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    case 64: hipLaunchKernelGGL(lspg_gram_kernel<4>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    case 96: hipLaunchKernelGGL(lspg_gram_kernel<6>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
+    case 32: hipLaunchKernelGGL(lspg_gram_mfma_kernel<2>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
+    case 64: hipLaunchKernelGGL(lspg_gram_mfma_kernel<4>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
+    case 96: hipLaunchKernelGGL(lspg_gram_mfma_kernel<6>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
     case 128: hipLaunchKernelGGL(lspg_gram_kernel<8>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
     default: return -1;
     }
-    hipLaunchKernelGGL(lspg_sum_kernel, dim3((P * P + kLB - 1) / kLB), dim3(kLB), 0, st,
-                       (const double *)partial, ng, (size_t)P * P, P * P, G);
+    // two-level deterministic reduction of the per-workgroup partials
+    const int PP = P * P;
+    double *mid = partial + (size_t)ng * PP;
+    hipLaunchKernelGGL(lspg_sum_kernel, dim3((PP + kLB - 1) / kLB, kSumSlices), dim3(kLB), 0, st,
+                       (const double *)partial, ng, (size_t)PP, PP, mid);
+    hipLaunchKernelGGL(lspg_sum_kernel, dim3((PP + kLB - 1) / kLB, 1), dim3(kLB), 0, st,
+                       (const double *)mid, kSumSlices, (size_t)PP, PP, G);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -302,11 +457,12 @@ int launch_lspg_solve(const double *G, int npod, double *y, double *dy, unsigned
                       hipStream_t st)
 {
     static bool attr = false;
-    const size_t lds = sizeof(double) * (size_t)npod * (npod + 1);
+    const size_t lds = sizeof(double) * (size_t)(npod + 1) * lspg_solve_ld(npod + 1);
     if (!attr) {
         if (hipFuncSetAttribute((const void *)lspg_solve_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)(sizeof(double) * kLspgMaxPod * (kLspgMaxPod + 1))) !=
+                                (int)(sizeof(double) * (kLspgMaxPod + 1) *
+                                      lspg_solve_ld(kLspgMaxPod + 1))) !=
             hipSuccess)
             return -3;
         attr = true;

@@ -16,4 +16,6 @@ cat $O/probe_1024.json
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/tools/lspg_probe.py 1024 95 5 > $O/prof.log 2>&1 || { tail -20 $O/prof.log; exit 1; }
 head -12 $O/prof/run_kernel_stats.csv
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d $O/pmc_fetch -o run -- python3 $R/tools/lspg_probe.py 1024 95 3 > $O/pmc_fetch.log 2>&1 || { tail -20 $O/pmc_fetch.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d $O/pmc_write -o run -- python3 $R/tools/lspg_probe.py 1024 95 3 > $O/pmc_write.log 2>&1 || { tail -20 $O/pmc_write.log; exit 1; }
 echo ALLOK
