@@ -67,7 +67,8 @@ def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
 def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
                                 snap_every=1, device=0, engine="pipe", tile_w=64,
                                 tol=DEFAULT_TOL, par_passes=0, verbose=1, allow_nonsquare=False,
-                                newton_max_its=100, newton_rtol=1e-12, return_stats=False):
+                                newton_max_its=100, newton_rtol=1e-12, return_stats=False,
+                                out=None):
     """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM
     (C/hypernet2D.py:72-131) on an MI355X.
 
@@ -79,14 +80,17 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
     Both return the reference's snapshot matrix.  verbose=1 prints the
     reference's header line; verbose=2 also the per-step lines
-    (" ... Working on timestep i" and Newton's "k: rel").
+    (" ... Working on timestep i" and Newton's "k: rel").  out: an existing
+    (2n, num_steps//snap_every + 1) C-contiguous float64 array (e.g. a .npy
+    memmap) the snapshots are written into and returned.
     """
     if verbose:
         print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mu, device, allow_nonsquare, tile_w=tile_w,
                    par_passes=par_passes, tol=tol, engine=engine)
     snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
-                                     solver, newton_max_its, newton_rtol, int(snap_every))
+                                     solver, newton_max_its, newton_rtol, int(snap_every),
+                                     out=out)
     if verbose >= 2:
         for i in range(int(num_steps)):
             print(" ... Working on timestep {}".format(i))
@@ -100,7 +104,7 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
 
 def inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps, mus, *, snap_every=1,
                                       device=0, verbose=1, allow_nonsquare=False,
-                                      return_stats=False):
+                                      return_stats=False, outs=None):
     """inviscid_burgers_implicit2D (C/hypernet2D.py:72-131) for a LIST of mu at
     once -- what the reference's drivers do one call at a time when they fill
     a snapshot set (C/run_prom.py:59-71 over the 9 get_snapshot_params,
@@ -114,7 +118,7 @@ def inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps, mus, *,
             print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mus[0], device, allow_nonsquare, engine="pipe")
     snaps, stats = ctx.sweep(mus, int(num_steps), w0=np.asarray(w0, dtype=np.float64).ravel(),
-                             snap_every=int(snap_every))
+                             snap_every=int(snap_every), outs=outs)
     if return_stats:
         return snaps, stats
     return snaps
@@ -260,31 +264,70 @@ def get_saved_params(snap_folder="param_snaps"):
     return set(glob.glob(snap_folder + "/*"))
 
 
+def _open_cache(fn, m, ncols):
+    """A .npy file of shape (m, ncols) float64 C-order (np.save's format),
+    memory-mapped for writing under a temporary name; _commit_cache renames it
+    once complete, so an interrupted run never leaves a truncated cache file
+    that get_saved_params would then trust."""
+    tmp = fn + ".partial.npy"
+    return tmp, np.lib.format.open_memmap(tmp, mode="w+", dtype=np.float64, shape=(m, ncols))
+
+
+def _commit_cache(tmp, fn, mm):
+    mm.flush()
+    del mm
+    os.replace(tmp, fn)
+
+
 def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="param_snaps",
-                          **solver_kw):
+                          stream=False, mmap=False, **solver_kw):
     """Load cached snapshots for mu, or compute and cache them
-    (C/hypernet2D.py:3111-3145).  solver_kw go to inviscid_burgers_implicit2D."""
+    (C/hypernet2D.py:3111-3145; same file names and .npy format, so caches
+    are interchangeable with the reference's).  solver_kw go to
+    inviscid_burgers_implicit2D.
+
+    stream=False (default): the reference's flow -- the snapshot matrix in
+    host memory (filled by pinned DMA from HBM), then np.save.  stream=True:
+    the library writes the snapshots straight into a memory map of the cache
+    file, so the host never holds the matrix twice (for trajectories that do
+    not fit host memory twice); the returned array is an in-memory copy
+    unless mmap=True (then the file's read-only memory map).  Measured at
+    1024^2 x 101 columns (1.7 GB, tools/snapio_probe.py):
+    0.29 s default vs 0.52 s streamed -- file-backed pages cannot be pinned,
+    so the streamed D2H runs at pageable speed.
+    mmap=True on a cache hit: np.load(..., mmap_mode='r') instead of reading
+    the whole file."""
     if not os.path.exists(snap_folder):
         os.makedirs(snap_folder)
     snap_fn = param_to_snap_fn(mu, snap_folder=snap_folder)
     if snap_fn in get_saved_params(snap_folder=snap_folder):
         print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
-        snaps = np.load(snap_fn)[:, :num_steps + 1]
-    else:
-        print(f"Computing new snaps for mu1={mu[0]}, mu2={mu[1]}")
-        t0 = time.time()
+        return np.load(snap_fn, mmap_mode="r" if mmap else None)[:, :num_steps + 1]
+    print(f"Computing new snaps for mu1={mu[0]}, mu2={mu[1]}")
+    t0 = time.time()
+    if not stream:
         snaps = inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, **solver_kw)
         print("Elapsed time: {:3.3e}".format(time.time() - t0))
         np.save(snap_fn, snaps)
-    return snaps
+        return snaps
+    m = np.asarray(w0).size
+    ncols = int(num_steps) // int(solver_kw.get("snap_every", 1)) + 1
+    tmp, mm = _open_cache(snap_fn, m, ncols)
+    inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, out=mm, **solver_kw)
+    print("Elapsed time: {:3.3e}".format(time.time() - t0))
+    snaps = None if mmap else np.array(mm)
+    _commit_cache(tmp, snap_fn, mm)
+    return np.load(snap_fn, mmap_mode="r") if mmap else snaps
 
 
 def load_or_compute_snaps_sweep(mus, grid_x, grid_y, w0, dt, num_steps,
-                                snap_folder="param_snaps"):
+                                snap_folder="param_snaps", stream=False, mmap=False):
     """load_or_compute_snaps (C/hypernet2D.py:3111-3145) for a list of mu: the
     cached ones are loaded, all missing ones are computed in ONE GPU sweep
     (inviscid_burgers_implicit2D_sweep) and cached under the reference's file
-    names.  Returns the list of snapshot matrices in the order of `mus`."""
+    names (streamed into the files' memory maps with stream=True, as in
+    load_or_compute_snaps).  Returns the list of snapshot matrices in the
+    order of `mus`."""
     if not os.path.exists(snap_folder):
         os.makedirs(snap_folder)
     saved = get_saved_params(snap_folder=snap_folder)
@@ -294,17 +337,28 @@ def load_or_compute_snaps_sweep(mus, grid_x, grid_y, w0, dt, num_steps,
         fn = param_to_snap_fn(mu, snap_folder=snap_folder)
         if fn in saved:
             print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
-            out[i] = np.load(fn)[:, :num_steps + 1]
+            out[i] = np.load(fn, mmap_mode="r" if mmap else None)[:, :num_steps + 1]
         else:
             todo.append(i)
     if todo:
         for i in todo:
             print(f"Computing new snaps for mu1={mus[i][0]}, mu2={mus[i][1]}")
         t0 = time.time()
+        fns = [param_to_snap_fn(mus[i], snap_folder=snap_folder) for i in todo]
+        caches = [_open_cache(fn, np.asarray(w0).size, int(num_steps) + 1) for fn in fns] \
+            if stream else None
         snaps = inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps,
-                                                  [mus[i] for i in todo], verbose=0)
+                                                  [mus[i] for i in todo], verbose=0,
+                                                  outs=[c[1] for c in caches] if stream else None)
         print("Elapsed time: {:3.3e}".format(time.time() - t0))
-        for i, sn in zip(todo, snaps):
-            np.save(param_to_snap_fn(mus[i], snap_folder=snap_folder), sn)
-            out[i] = sn
+        for k, (i, sn) in enumerate(zip(todo, snaps)):
+            if stream:
+                tmp, mm = caches[k]
+                keep = None if mmap else np.array(mm)
+                del sn
+                _commit_cache(tmp, fns[k], mm)
+                out[i] = np.load(fns[k], mmap_mode="r") if mmap else keep
+            else:
+                np.save(fns[k], sn)
+                out[i] = sn
     return out

@@ -122,12 +122,15 @@ class FOMContext:
 
     # ---- time loop --------------------------------------------------------
     def run(self, w0, num_steps, solver="march", newton_max_its=100, newton_rtol=1e-12,
-            snap_every=1, keep_snaps=True):
+            snap_every=1, keep_snaps=True, out=None):
         """Returns (snaps (m, num_steps//snap_every + 1) C-order or None,
-        stats dict, per-step iterations int32[num_steps], per-step rel[num_steps])."""
+        stats dict, per-step iterations int32[num_steps], per-step rel[num_steps]).
+        out: an existing C-contiguous float64 (m, ncols) array to fill instead
+        of a new one -- e.g. np.lib.format.open_memmap of the snapshot cache
+        file, so the snapshots stream from HBM into the .npy file's pages."""
         w0 = self._vec(w0, "w0")
         ncols = num_steps // snap_every + 1
-        snaps = np.zeros((self.m, ncols)) if keep_snaps else None
+        snaps = _out_array(out, self.m, ncols) if keep_snaps else None
         its = np.zeros(num_steps, dtype=np.int32)
         rel = np.zeros(num_steps)
         st = _lib.BurgStats()
@@ -158,13 +161,15 @@ class FOMContext:
                                            ctypes.byref(st)))
         return st.as_dict()
 
-    def sweep(self, mus, num_steps, w0=None, keep_snaps=True, snap_every=1):
+    def sweep(self, mus, num_steps, w0=None, keep_snaps=True, snap_every=1, outs=None):
         """Parameter sweep (burg_sweep): one trajectory of num_steps steps per
         mu in `mus`, all from w0 (None: the state last passed to upload()),
         on the grid and dt of the last set_problem, back to back in one
         pipelined launch per group of trajectories.  Returns (list of snapshot
         matrices (m, num_steps//snap_every + 1), or None with
-        keep_snaps=False -- then the states stay in HBM --, stats)."""
+        keep_snaps=False -- then the states stay in HBM --, stats).  outs: a
+        list of existing (m, ncols) C-contiguous float64 arrays (None entries:
+        allocate) to fill, as run()'s out."""
         if getattr(self, "_grid", None) is None:
             raise RuntimeError("set_problem first")
         gx, gy, dt, nonsq = self._grid
@@ -184,7 +189,10 @@ class FOMContext:
         snaps = None
         ptrs = None
         if keep_snaps:
-            snaps = [np.zeros((self.m, ncols)) for _ in mus]
+            outs = list(outs) if outs is not None else [None] * len(mus)
+            if len(outs) != len(mus):
+                raise ValueError("outs must have one entry per mu")
+            snaps = [_out_array(o, self.m, ncols) for o in outs]
             ptrs = (_lib._D * len(mus))(*[_lib.dptr(a) for a in snaps])
         st = _lib.BurgStats()
         _lib.check(self._L.burg_sweep(self._h, len(mus), _lib.dptr(src_b), _lib.dptr(lbc_b),
@@ -252,6 +260,15 @@ class FOMContext:
         _lib.check(self._L.burg_advance(self._h, int(num_steps), _lib.SOLVERS[solver],
                                         ctypes.byref(st)), allow=())
         return st.as_dict()
+
+
+def _out_array(out, m, ncols):
+    if out is None:
+        return np.zeros((m, ncols))
+    if (not isinstance(out, np.ndarray) or out.dtype != np.float64 or out.shape != (m, ncols)
+            or not out.flags.c_contiguous or not out.flags.writeable):
+        raise ValueError(f"out must be a writeable C-contiguous float64 ({m}, {ncols}) array")
+    return out
 
 
 _cache = threading.local()

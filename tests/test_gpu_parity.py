@@ -562,3 +562,39 @@ def test_lspg_step_counts_and_rank_errors(gpu, orc):
     sq = make_ctx(N, ny=N + 3)
     with pytest.raises(_lib.BurgersError):
         sq.lspg(np.ones(2 * N * (N + 3)), 1, np.ones((2 * N * (N + 3), 2)))
+
+
+def test_streamed_snapshot_cache(gpu, tmp_path):
+    """load_or_compute_snaps(stream=True) writes the snapshots from HBM straight
+    into a memory map of the cache file: same file (np.save format, reference
+    name) and same array as the reference's array-then-np.save flow
+    (stream=False); no partial file left; mmap=True hands back the map."""
+    from finitedifference_amd import hypernet2D as H
+    N, T = 64, 9
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    w0 = np.ones(2 * N * N)
+    mu = (4.56, 0.019)
+    a = H.load_or_compute_snaps(mu, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "s"),
+                                stream=True)
+    b = H.load_or_compute_snaps(mu, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "n"),
+                                stream=False)
+    assert np.array_equal(a, b) and a.shape == (2 * N * N, T + 1)
+    fa = H.param_to_snap_fn(mu, str(tmp_path / "s"))
+    fb = H.param_to_snap_fn(mu, str(tmp_path / "n"))
+    assert open(fa, "rb").read() == open(fb, "rb").read()
+    assert sorted(os.listdir(tmp_path / "s")) == [os.path.basename(fa)]
+    c = H.load_or_compute_snaps(mu, gx, gy, w0, 0.05, 5, snap_folder=str(tmp_path / "s"), mmap=True)
+    assert isinstance(c.base, np.memmap) or isinstance(c, np.memmap)
+    assert np.array_equal(c, a[:, :6])
+    d = H.load_or_compute_snaps(mu, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "m"),
+                                stream=True, mmap=True)
+    assert np.array_equal(d, a)
+    mus = SWEEP_MUS[:3]
+    sw = H.load_or_compute_snaps_sweep(mus, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "w"),
+                                       stream=True)
+    sn = H.load_or_compute_snaps_sweep(mus, gx, gy, w0, 0.05, T, snap_folder=str(tmp_path / "x"),
+                                       stream=False)
+    for x, y, mu_ in zip(sw, sn, mus):
+        assert np.array_equal(x, y)
+        assert (open(H.param_to_snap_fn(mu_, str(tmp_path / "w")), "rb").read() ==
+                open(H.param_to_snap_fn(mu_, str(tmp_path / "x")), "rb").read())

@@ -66,3 +66,16 @@ def test_slab_rows_partition(ny, world):
     for (a0, n0), (a1, n1) in zip(parts, parts[1:]):
         assert a0 + n0 == a1 and abs(n0 - n1) <= 1
     assert parts[-1][0] + parts[-1][1] == ny
+
+
+def test_cache_memmap_commit_is_np_save_format(tmp_path):
+    """The streamed cache (hypernet2D._open_cache / _commit_cache) produces the
+    exact bytes np.save writes for the same array (C/hypernet2D.py:3143)."""
+    a = np.random.default_rng(3).random((6, 5))
+    fn = str(tmp_path / "mu1_1.0+mu2_2.0.npy")
+    tmp, mm = hn._open_cache(fn, 6, 5)
+    mm[...] = a
+    hn._commit_cache(tmp, fn, mm)
+    np.save(str(tmp_path / "ref.npy"), a)
+    assert open(fn, "rb").read() == open(str(tmp_path / "ref.npy"), "rb").read()
+    assert not os.path.exists(tmp)

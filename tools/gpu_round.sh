@@ -1,0 +1,18 @@
+#!/bin/bash
+# Full GPU pass (under gpurun): every GPU test, smoke, default bench, the LSPG
+# and snapshot-I/O probes.
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${TAG:-round}
+mkdir -p $O
+cd $R
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+cat $O/smoke.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 300 python tools/snapio_probe.py 1024 100 /tmp/snapio > $O/snapio_1024.json 2> $O/snapio.err || { tail -20 $O/snapio.err; exit 1; }
+cat $O/snapio_1024.json
+echo ALLOK
