@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -27,6 +27,7 @@ EXPORTS = (
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_lspg",
+    "burg_pod",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -125,6 +126,8 @@ def load(path=None):
                                          ctypes.c_double, ctypes.c_double, _D, ctypes.c_int64,
                                          _D, ctypes.c_int64, _I32, _D, _D,
                                          ctypes.POINTER(BurgStats)]),
+            "burg_pod": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, _D,
+                                        ctypes.c_int, _D, _D, _D]),
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),

@@ -1771,4 +1771,59 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     return rc;
 }
 
+int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *U, double *sigma,
+             double *ms)
+{
+    if (!snaps || !U || !sigma) return fail(BURG_EINVAL, "null array");
+    if (m < 1 || ns < 1 || k < 1 || k > ns)
+        return fail(BURG_EINVAL, "burg_pod: need m, ns >= 1 and 1 <= k <= ns (m=%lld ns=%d k=%d)",
+                    (long long)m, ns, k);
+    HIPCHK(hipSetDevice(device));
+    hipStream_t st = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    double *d_s = nullptr, *d_u = nullptr, *d_sig = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        dfree(d_s), dfree(d_u), dfree(d_sig);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        (void)hipStreamDestroy(st);
+    };
+    const size_t mm = (size_t)m;
+    int rc = BURG_OK;
+    if ((rc = dalloc(&d_s, mm * ns)) || (rc = dalloc(&d_u, mm * k)) || (rc = dalloc(&d_sig, (size_t)k))) {
+        cleanup();
+        return rc;
+    }
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    if (hipMemcpyAsync(d_s, snaps, sizeof(double) * mm * ns, hipMemcpyHostToDevice, st) != hipSuccess) {
+        cleanup();
+        return fail(BURG_EHIP, "burg_pod: snapshot upload failed");
+    }
+    (void)hipEventRecord(e0, st);
+    char msg[256] = {0};
+    const int r = pod_device(st, mm, ns, d_s, k, d_u, d_sig, msg, sizeof msg);
+    (void)hipEventRecord(e1, st);
+    if (r != 0) {
+        cleanup();
+        return fail(r == -1 ? BURG_EINVAL : r == -5 ? BURG_ENOMEM : r == -6 ? BURG_ENOCONV : BURG_EHIP,
+                    "burg_pod: %s", msg);
+    }
+    if (hipMemcpyAsync(U, d_u, sizeof(double) * mm * k, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(sigma, d_sig, sizeof(double) * k, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return fail(BURG_EHIP, "burg_pod: result download failed");
+    }
+    if (ms) {
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, e0, e1);
+        *ms = t;
+    }
+    cleanup();
+    return BURG_OK;
+}
+
 }  // extern "C"

@@ -1,0 +1,180 @@
+// pod.hip -- POD of a snapshot matrix on the GPU (SURVEY.md section 8(f),
+// row 4): POD(snaps, num_modes, method), C/hypernet2D.py:2670-2695, as called
+// by C/run_prom.py:58-86 on the (2n, 9 x 501) training snapshot set.
+//
+// The reference calls np.linalg.svd (method 'svd') or sklearn's
+// randomized_svd (method 'rsvd', unseeded).  Here: the exact thin SVD by
+// Householder QR of the tall snapshot matrix and an SVD of its small R factor,
+//     S = Q R,  R = U_R Sigma V^T,  U = Q [U_R; 0]
+// all with rocSOLVER on the device (dgeqrf, dgesvd, dormqr), so the basis
+// keeps LAPACK's backward stability (the method of snapshots, eig(S^T S),
+// would square the condition number and lose the trailing modes).  The
+// host's C-order (m x ns) matrix is a column-major (ns x m) one, so it is
+// transposed once on the device (basis_transpose_kernel, ecsw.hip); the
+// result is transposed back into C-order (m x k).  Signs: each column is
+// flipped so that its largest-magnitude entry is positive (sklearn's
+// svd_flip rule on U) -- LAPACK's signs are arbitrary.
+#include "burg_internal.h"
+
+#include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
+
+namespace burg {
+namespace {
+
+constexpr int kPB = 256;
+
+// R (upper triangle of the QR factor, column-major lda) -> dense ns x ns
+__global__ __launch_bounds__(kPB) void triu_copy_kernel(const double *__restrict__ a, size_t lda,
+                                                        int ns, double *__restrict__ r)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= (size_t)ns * ns) return;
+    const int col = (int)(e / ns), row = (int)(e % ns);
+    r[e] = row <= col ? a[(size_t)col * lda + row] : 0.0;
+}
+
+// C (m x k column-major, ldc = m) <- [U_R[:, :k]; 0]
+__global__ __launch_bounds__(kPB) void embed_kernel(const double *__restrict__ ur, int ns, int k,
+                                                    size_t m, double *__restrict__ c)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= m * k) return;
+    const size_t col = e / m, row = e % m;
+    c[e] = row < (size_t)ns ? ur[col * ns + row] : 0.0;
+}
+
+// per column of C (m x k column-major): sign of its largest-|.| entry
+__global__ __launch_bounds__(kPB) void col_sign_kernel(const double *__restrict__ c, size_t m,
+                                                       double *__restrict__ sgn)
+{
+    const double *p = c + (size_t)blockIdx.x * m;
+    double best = -1.0, val = 0.0;
+    for (size_t i = threadIdx.x; i < m; i += kPB) {
+        const double a = fabs(p[i]);
+        if (a > best) best = a, val = p[i];
+    }
+    __shared__ double bb[kPB], bv[kPB];
+    bb[threadIdx.x] = best;
+    bv[threadIdx.x] = val;
+    __syncthreads();
+    for (int h = kPB / 2; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h && bb[threadIdx.x + h] > bb[threadIdx.x]) {
+            bb[threadIdx.x] = bb[threadIdx.x + h];
+            bv[threadIdx.x] = bv[threadIdx.x + h];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) sgn[blockIdx.x] = bv[0] < 0.0 ? -1.0 : 1.0;
+}
+
+__global__ __launch_bounds__(kPB) void col_scale_kernel(double *__restrict__ c, size_t m, int k,
+                                                        const double *__restrict__ sgn)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= m * k) return;
+    c[e] *= sgn[e / m];
+}
+
+unsigned blocks(size_t n) { return (unsigned)((n + kPB - 1) / kPB); }
+
+}  // namespace
+
+int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, double *d_u,
+               double *d_sigma, char *msg, size_t msglen)
+{
+    // d_s: C-order (m x ns) snapshots on the device; d_u: C-order (m x k) out
+    auto err = [&](const char *what, int code) {
+        snprintf(msg, msglen, "%s failed (%d)", what, code);
+        return -3;
+    };
+    if (m < (size_t)ns) {
+        snprintf(msg, msglen, "POD needs at least as many rows as snapshots (m=%zu < ns=%d)", m, ns);
+        return -1;
+    }
+    if (m > 0x7fffffffULL) {
+        snprintf(msg, msglen, "m=%zu exceeds rocSOLVER's 32-bit sizes", m);
+        return -1;
+    }
+    double *a = nullptr, *tau = nullptr, *r = nullptr, *ur = nullptr, *e = nullptr, *c = nullptr,
+           *sgn = nullptr, *sv = nullptr;
+    rocblas_int *info = nullptr;
+    rocblas_handle h = nullptr;
+    int rc = 0;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        if (h) rocblas_destroy_handle(h);
+        for (double *p : {a, tau, r, ur, e, c, sgn, sv})
+            if (p) (void)hipFree(p);
+        if (info) (void)hipFree(info);
+    };
+    const size_t nsz = (size_t)ns;
+    if (hipMalloc(&a, sizeof(double) * m * nsz) != hipSuccess ||
+        hipMalloc(&tau, sizeof(double) * nsz) != hipSuccess ||
+        hipMalloc(&r, sizeof(double) * nsz * nsz) != hipSuccess ||
+        hipMalloc(&ur, sizeof(double) * nsz * nsz) != hipSuccess ||
+        hipMalloc(&e, sizeof(double) * nsz) != hipSuccess ||
+        hipMalloc(&sv, sizeof(double) * nsz) != hipSuccess ||
+        hipMalloc(&c, sizeof(double) * m * k) != hipSuccess ||
+        hipMalloc(&sgn, sizeof(double) * k) != hipSuccess ||
+        hipMalloc(&info, sizeof(rocblas_int)) != hipSuccess) {
+        cleanup();
+        snprintf(msg, msglen, "POD: hipMalloc of %zu MB failed",
+                 (size_t)((sizeof(double) * (m * nsz + m * k + 2 * nsz * nsz)) >> 20));
+        return -5;
+    }
+    if (rocblas_create_handle(&h) != rocblas_status_success) {
+        cleanup();
+        return err("rocblas_create_handle", 0);
+    }
+    rocblas_set_stream(h, st);
+    // column-major (m x ns) copy of the snapshots
+    if ((rc = launch_basis_transpose(d_s, a, m, ns, st))) {
+        cleanup();
+        return err("transpose", rc);
+    }
+    rocblas_status s;
+    if ((s = rocsolver_dgeqrf(h, (rocblas_int)m, ns, a, (rocblas_int)m, tau)) !=
+        rocblas_status_success) {
+        cleanup();
+        return err("rocsolver_dgeqrf", (int)s);
+    }
+    hipLaunchKernelGGL(triu_copy_kernel, dim3(blocks(nsz * nsz)), dim3(kPB), 0, st, a, m, ns, r);
+    if ((s = rocsolver_dgesvd(h, rocblas_svect_singular, rocblas_svect_none, ns, ns, r, ns, sv, ur,
+                              ns, nullptr, 1, e, rocblas_outofplace, info)) !=
+        rocblas_status_success) {
+        cleanup();
+        return err("rocsolver_dgesvd", (int)s);
+    }
+    hipLaunchKernelGGL(embed_kernel, dim3(blocks(m * k)), dim3(kPB), 0, st, ur, ns, k, m, c);
+    if ((s = rocsolver_dormqr(h, rocblas_side_left, rocblas_operation_none, (rocblas_int)m, k, ns,
+                              a, (rocblas_int)m, tau, c, (rocblas_int)m)) !=
+        rocblas_status_success) {
+        cleanup();
+        return err("rocsolver_dormqr", (int)s);
+    }
+    hipLaunchKernelGGL(col_sign_kernel, dim3(k), dim3(kPB), 0, st, c, m, sgn);
+    hipLaunchKernelGGL(col_scale_kernel, dim3(blocks(m * k)), dim3(kPB), 0, st, c, m, k,
+                       (const double *)sgn);
+    // column-major (m x k) = C-order (k x m) -> C-order (m x k)
+    if ((rc = launch_basis_transpose(c, d_u, (size_t)k, (int)m, st))) {
+        cleanup();
+        return err("transpose back", rc);
+    }
+    (void)hipMemcpyAsync(d_sigma, sv, sizeof(double) * k, hipMemcpyDeviceToDevice, st);
+    rocblas_int hinfo = 0;
+    (void)hipMemcpyAsync(&hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return err("POD stream", 0);
+    }
+    cleanup();
+    if (hinfo != 0) {
+        snprintf(msg, msglen, "rocsolver_dgesvd did not converge (info=%d)", (int)hinfo);
+        return -6;
+    }
+    return 0;
+}
+
+}  // namespace burg

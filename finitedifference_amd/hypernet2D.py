@@ -21,6 +21,7 @@ num_steps + 1), C-contiguous, column j = state after j steps, u rows then v
 rows.  Extensions are keyword-only (solver, snap_every, device, tile_w, tol,
 par_passes, verbose, allow_nonsquare) and default to reference behaviour.
 """
+import ctypes
 import glob
 import os
 import time
@@ -239,6 +240,37 @@ def inviscid_burgers_implicit2D_LSPG(grid_x, grid_y, w0, dt, num_steps, mu, basi
             print("iteration {}: relative norm {:3.2e}".format(int(its[i]) - 1, rel[i]))
     out = (snaps, (int(its.sum()), times[0] / 1e3, times[1] / 1e3, times[2] / 1e3))
     return out + (red,) if return_coords else out
+
+
+def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, return_ms=False):
+    """POD of a snapshot matrix (C/hypernet2D.py:2670-2695) on the GPU
+    (burg_pod: Householder QR of the tall matrix, SVD of R, Q applied to the
+    R-factor's singular vectors -- rocSOLVER, backward stable like LAPACK).
+    Returns (u, s) as the reference: method 'svd' -> all min(m, ns) modes
+    (np.linalg.svd(snaps, full_matrices=False), num_modes unused as there);
+    method 'rsvd' -> num_modes modes (default all).  'rsvd' returns the EXACT
+    truncated SVD that sklearn's randomized_svd approximates (the reference
+    calls it unseeded, so it has no reproducible output to match);
+    random_state is accepted and ignored.  Column signs follow sklearn's
+    svd_flip rule on u (largest-magnitude entry positive); np.linalg.svd's are
+    arbitrary."""
+    if method not in ("svd", "rsvd"):
+        raise ValueError("Unknown method '{}' for POD. Use 'svd' or 'rsvd'.".format(method))
+    from . import _lib
+    S = np.ascontiguousarray(np.asarray(snaps, dtype=np.float64))
+    if S.ndim != 2:
+        raise ValueError("snaps must be a 2-D (dofs, snapshots) matrix")
+    m, ns = S.shape
+    if m < ns:
+        raise ValueError("POD on the GPU needs at least as many rows as snapshots")
+    k = min(m, ns) if (method == "svd" or num_modes is None) else int(num_modes)
+    u = np.zeros((m, k))
+    sv = np.zeros(k)
+    ms = ctypes.c_double(0.0)
+    L = _lib.load()
+    _lib.check(L.burg_pod(int(device), m, ns, _lib.dptr(S), k, _lib.dptr(u), _lib.dptr(sv),
+                          ctypes.byref(ms)))
+    return (u, sv, ms.value) if return_ms else (u, sv)
 
 
 def compute_error(rom_snaps, hdm_snaps):

@@ -20,6 +20,7 @@
  *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
  *   burg_lspg           C/hypernet2D.py:133-200   inviscid_burgers_implicit2D_LSPG
  *                       with C/hypernet2D.py:1859-1929 gauss_newton_LSPG
+ *   burg_pod            C/hypernet2D.py:2670-2695   POD (np.linalg.svd / randomized_svd)
  *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
  *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
  *
@@ -42,7 +43,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 5
+#define BURG_ABI_VERSION 6
 
 enum burg_status {
     BURG_OK = 0,
@@ -248,6 +249,17 @@ int burg_lspg(burg_ctx *ctx, const double *w0, int num_steps, int n_pod, const d
               int max_its, double relnorm_cutoff, double min_delta, double *snaps,
               int64_t ld_snaps, double *red_coords, int64_t ld_red, int32_t *step_its,
               double *step_rel, double *times_ms, burg_stats *stats);
+
+/* POD of a snapshot matrix (POD, C/hypernet2D.py:2670-2695, as run_prom.py:58-86
+ * calls it): the exact thin SVD S = U diag(sigma) V^T by Householder QR of S
+ * and an SVD of its R factor (rocSOLVER dgeqrf / dgesvd / dormqr on the
+ * device).  snaps: (m x ns) C-order host matrix, m >= ns; U: (m x k) C-order
+ * host output, the k leading left singular vectors, each column's
+ * largest-magnitude entry made positive (sklearn's svd_flip rule); sigma: k
+ * singular values, descending.  1 <= k <= ns.  ms (may be NULL): device time
+ * of the factorisation (HIP events).  No context: runs on `device`. */
+int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *U, double *sigma,
+             double *ms);
 
 #ifdef __cplusplus
 }

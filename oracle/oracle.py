@@ -211,6 +211,22 @@ class Problem:
         return snaps, its, rels
 
 
+def svd_flip_u(u):
+    """sklearn's svd_flip rule on u: each column's largest-|.| entry positive."""
+    idx = np.argmax(np.abs(u), axis=0)
+    sg = np.sign(u[idx, np.arange(u.shape[1])])
+    sg[sg == 0] = 1.0
+    return u * sg
+
+
+def pod_svd(snaps):
+    """POD(snaps, method='svd') (C/hypernet2D.py:2670-2695) restated: the thin
+    SVD np.linalg.svd(snaps, full_matrices=False) -> (u, s), u's column signs
+    normalised by svd_flip_u (LAPACK's are arbitrary)."""
+    u, s, _ = np.linalg.svd(np.asarray(snaps, dtype=np.float64), full_matrices=False)
+    return svd_flip_u(u), s
+
+
 def rel_l2(a, b):
     a, b = np.asarray(a), np.asarray(b)
     return float(np.linalg.norm(a - b) / np.linalg.norm(b))

@@ -33,6 +33,8 @@ Fixtures written
                      (from its printed 'iteration i' lines), and the LSPG
                      Jacobian (row-only JDyec permutation, :165-167) times the
                      basis at a random state
+  ref_pod.npz        POD (:2670-2695) of reference snapshot sets: method 'svd'
+                     (u, s) and method 'rsvd' with random_state=0 (10 modes)
   author_logs.json   Newton counts/residuals from the author's SLURM log
                      F/output_55034725.log (750^2)
 """
@@ -196,6 +198,19 @@ def make_lspg(hn):
     np.savez_compressed(os.path.join(HERE, "ref_lspg.npz"), **out)
 
 
+def make_pod(hn):
+    out = {}
+    for tag, N, T, mus in (("n16", 16, 30, ((4.25, 0.015), (5.5, 0.03))),
+                           ("n24", 24, 20, ((4.25, 0.015), (5.5, 0.03), (5.19, 0.026)))):
+        S = np.hstack([run_reference(hn, N, T, m)[0] for m in mus])
+        u, s = hn.POD(S, method="svd")
+        ur, sr = hn.POD(S, num_modes=10, method="rsvd", random_state=0)
+        out.update({f"{tag}_S": S, f"{tag}_u": u, f"{tag}_s": s, f"{tag}_ur": ur,
+                    f"{tag}_sr": sr})
+        print(f"pod {tag}: S {S.shape}, s[0] {s[0]:.6e}, s[-1] {s[-1]:.3e}")
+    np.savez_compressed(os.path.join(HERE, "ref_pod.npz"), **out)
+
+
 def _summaries(snaps, N, steps_full):
     n = N * N
     T1 = snaps.shape[1]
@@ -319,6 +334,8 @@ def main():
             make_ops(hn)
         if not only or "ecsw" in only:
             make_ecsw(hn)
+        if not only or "pod" in only:
+            make_pod(hn)
         if not only or "lspg" in only:
             make_lspg(hn)
         if not only or "coarse" in only:

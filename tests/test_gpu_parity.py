@@ -598,3 +598,61 @@ def test_streamed_snapshot_cache(gpu, tmp_path):
         assert np.array_equal(x, y)
         assert (open(H.param_to_snap_fn(mu_, str(tmp_path / "w")), "rb").read() ==
                 open(H.param_to_snap_fn(mu_, str(tmp_path / "x")), "rb").read())
+
+
+# ----------------------------------------------------- POD --
+def _pod_mode_mask(s, rel_floor=1e-6, rel_gap=1e-6):
+    """modes the SVD determines to ~1e-10: not noise, separated from neighbours"""
+    gap = np.full(s.size, np.inf)
+    gap[:-1] = np.minimum(gap[:-1], s[:-1] - s[1:])
+    gap[1:] = np.minimum(gap[1:], s[:-1] - s[1:])
+    return (s > rel_floor * s[0]) & (gap > rel_gap * s[0])
+
+
+@pytest.mark.parametrize("tag", ["n16", "n24"])
+def test_pod_vs_reference_and_oracle(gpu, orc, tag):
+    """POD on the GPU (burg_pod: rocSOLVER QR + SVD of R) against the
+    reference's np.linalg.svd output and sklearn's seeded randomized_svd
+    (tests/golden/ref_pod.npz).  Bars: singular values to 1e-12 of s[0];
+    well-determined modes (above 1e-6 s[0], gaps above 1e-6 s[0]) to 1e-8
+    after sign normalisation; U orthonormal; S reproduced by U U^T S."""
+    from finitedifference_amd import hypernet2D as H
+    g = golden("ref_pod.npz")
+    S = g[f"{tag}_S"]
+    u, s = H.POD(S, method="svd")
+    assert u.shape == g[f"{tag}_u"].shape and s.shape == g[f"{tag}_s"].shape
+    assert np.allclose(s, g[f"{tag}_s"], rtol=0, atol=1e-12 * s[0])
+    ur = orc.svd_flip_u(g[f"{tag}_u"])
+    keep = _pod_mode_mask(g[f"{tag}_s"])
+    assert keep.sum() >= 8
+    assert np.max(np.abs(u[:, keep] - ur[:, keep])) < 1e-8
+    assert np.max(np.abs(u.T @ u - np.eye(u.shape[1]))) < 1e-12
+    assert rel(u @ (u.T @ S), S) < 1e-13
+    uo, so = orc.pod_svd(S)
+    assert np.max(np.abs(u[:, keep] - uo[:, keep])) < 1e-8
+    u10, s10 = H.POD(S, num_modes=10, method="rsvd")
+    assert u10.shape == (S.shape[0], 10)
+    assert np.allclose(s10, g[f"{tag}_sr"], rtol=1e-8, atol=0)
+    assert np.all(np.abs(np.sum(u10 * g[f"{tag}_ur"], axis=0)) > 1 - 1e-8)
+
+
+def test_pod_tall_ragged_and_errors(gpu):
+    """A tall matrix with sizes off every tile (m = 2*37^2, ns = 45) against
+    numpy's SVD, and the error paths (k out of range, wide matrix)."""
+    from finitedifference_amd import _lib
+    from finitedifference_amd import hypernet2D as H
+    rng = np.random.default_rng(11)
+    m, ns = 2 * 37 * 37, 45
+    S = rng.standard_normal((m, 8)) @ rng.standard_normal((8, ns)) + 1e-3 * rng.standard_normal((m, ns))
+    u, s = H.POD(S, num_modes=20, method="rsvd")
+    un, sn, _ = np.linalg.svd(S, full_matrices=False)
+    assert np.allclose(s, sn[:20], rtol=1e-12)
+    keep = _pod_mode_mask(sn[:20], rel_floor=1e-12, rel_gap=1e-8)
+    assert np.all(np.abs(np.sum(u[:, keep] * un[:, :20][:, keep], axis=0)) > 1 - 1e-9)
+    with pytest.raises(ValueError):
+        H.POD(S.T)
+    L = _lib.load()
+    out = np.zeros((m, 1))
+    sv = np.zeros(1)
+    assert L.burg_pod(0, m, ns, _lib.dptr(np.ascontiguousarray(S)), 0, _lib.dptr(out),
+                      _lib.dptr(sv), None) == _lib.BURG_EINVAL

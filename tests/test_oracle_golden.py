@@ -221,3 +221,18 @@ def test_oracle_lspg_vs_reference(orc, tag):
     assert orc.rel_l2(snaps, g[f"{tag}_snaps"]) < 1e-13
     assert np.array_equal(its, g[f"{tag}_its"])
     assert np.allclose(rels, g[f"{tag}_rel"], rtol=1e-2)
+
+
+# ------------------------------------------------------- POD --
+@pytest.mark.parametrize("tag", ["n16", "n24"])
+def test_oracle_pod_vs_reference(orc, tag):
+    """oracle.pod_svd restates POD(method='svd') (C/hypernet2D.py:2670-2695);
+    against the reference's own output (tests/golden/ref_pod.npz), signs
+    normalised on both sides."""
+    g = golden("ref_pod.npz")
+    u, s = orc.pod_svd(g[f"{tag}_S"])
+    assert np.allclose(s, g[f"{tag}_s"], rtol=0, atol=1e-12 * s[0])
+    ur = orc.svd_flip_u(g[f"{tag}_u"])
+    keep = s > 1e-6 * s[0]
+    assert keep.sum() >= 8
+    assert np.max(np.abs(u[:, keep] - ur[:, keep])) < 1e-8
