@@ -199,6 +199,9 @@ int launch_lspg_solve(const double *G, int npod, double *y, double *dy, unsigned
 // rocSOLVER QR + SVD of R; U (m x k, C-order) and the k leading singular values
 int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, double *d_u,
                double *d_sigma, char *msg, size_t msglen);
+int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
+                    int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,
+                    size_t msglen);
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
                      int ldo, hipStream_t st);
 

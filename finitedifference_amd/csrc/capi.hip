@@ -1774,18 +1774,26 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
 int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *U, double *sigma,
              double *ms)
 {
+    return burg_pod_rsvd(device, m, ns, snaps, k, 0, 0, nullptr, U, sigma, ms);
+}
+
+int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
+                  const double *omega, double *U, double *sigma, double *ms)
+{
     if (!snaps || !U || !sigma) return fail(BURG_EINVAL, "null array");
+    if (omega && (nrand < k || nrand > ns || n_iter < 0))
+        return fail(BURG_EINVAL, "burg_pod_rsvd: need k <= nrand <= ns and n_iter >= 0");
     if (m < 1 || ns < 1 || k < 1 || k > ns)
         return fail(BURG_EINVAL, "burg_pod: need m, ns >= 1 and 1 <= k <= ns (m=%lld ns=%d k=%d)",
                     (long long)m, ns, k);
     HIPCHK(hipSetDevice(device));
     hipStream_t st = nullptr;
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    double *d_s = nullptr, *d_u = nullptr, *d_sig = nullptr;
+    double *d_s = nullptr, *d_u = nullptr, *d_sig = nullptr, *d_om = nullptr;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     auto cleanup = [&]() {
         (void)hipStreamSynchronize(st);
-        dfree(d_s), dfree(d_u), dfree(d_sig);
+        dfree(d_s), dfree(d_u), dfree(d_sig), dfree(d_om);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
         (void)hipStreamDestroy(st);
@@ -1802,9 +1810,22 @@ int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *
         cleanup();
         return fail(BURG_EHIP, "burg_pod: snapshot upload failed");
     }
+    if (omega) {
+        if ((rc = dalloc(&d_om, (size_t)ns * nrand))) {
+            cleanup();
+            return rc;
+        }
+        if (hipMemcpyAsync(d_om, omega, sizeof(double) * ns * nrand, hipMemcpyHostToDevice, st) !=
+            hipSuccess) {
+            cleanup();
+            return fail(BURG_EHIP, "burg_pod_rsvd: omega upload failed");
+        }
+    }
     (void)hipEventRecord(e0, st);
     char msg[256] = {0};
-    const int r = pod_device(st, mm, ns, d_s, k, d_u, d_sig, msg, sizeof msg);
+    const int r = omega ? pod_rsvd_device(st, mm, ns, d_s, k, nrand, n_iter, d_om, d_u, d_sig, msg,
+                                          sizeof msg)
+                        : pod_device(st, mm, ns, d_s, k, d_u, d_sig, msg, sizeof msg);
     (void)hipEventRecord(e1, st);
     if (r != 0) {
         cleanup();

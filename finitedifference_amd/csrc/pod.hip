@@ -177,4 +177,113 @@ int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, doubl
     return 0;
 }
 
+// Randomized truncated SVD (the algorithm of sklearn's randomized_svd, which
+// the reference's POD(method='rsvd') calls, C/hypernet2D.py:2688-2692):
+// Y = S Omega, n_iter power iterations Y <- orth(S orth(S^T Y)), Q = orth(Y),
+// B = Q^T S, B = U_B Sigma V^T, U = Q U_B[:, :k].  Orthonormalisation by
+// Householder QR (dgeqrf + dorgqr; sklearn's 'auto' normaliser is LU, which
+// spans the same subspace).  Every product is a rocBLAS dgemm on the device.
+// omega: (ns x nrand) column-major (host), k <= nrand <= ns.
+int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
+                    int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,
+                    size_t msglen)
+{
+    auto err = [&](const char *what, int code) {
+        snprintf(msg, msglen, "%s failed (%d)", what, code);
+        return -3;
+    };
+    if (m < (size_t)ns || m > 0x7fffffffULL || nrand < k || nrand > ns) {
+        snprintf(msg, msglen, "rsvd: need ns <= m < 2^31 and k <= nrand <= ns");
+        return -1;
+    }
+    const rocblas_int M = (rocblas_int)m, NS = ns, R = nrand;
+    double *a = nullptr, *y = nullptr, *z = nullptr, *tau = nullptr, *b = nullptr, *ub = nullptr,
+           *sv = nullptr, *e = nullptr, *c = nullptr, *sgn = nullptr;
+    rocblas_int *info = nullptr;
+    rocblas_handle h = nullptr;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        if (h) rocblas_destroy_handle(h);
+        for (double *p : {a, y, z, tau, b, ub, sv, e, c, sgn})
+            if (p) (void)hipFree(p);
+        if (info) (void)hipFree(info);
+    };
+    const size_t nsz = (size_t)ns;
+    if (hipMalloc(&a, sizeof(double) * m * nsz) != hipSuccess ||
+        hipMalloc(&y, sizeof(double) * m * R) != hipSuccess ||
+        hipMalloc(&z, sizeof(double) * nsz * R) != hipSuccess ||
+        hipMalloc(&tau, sizeof(double) * R) != hipSuccess ||
+        hipMalloc(&b, sizeof(double) * (size_t)R * nsz) != hipSuccess ||
+        hipMalloc(&ub, sizeof(double) * (size_t)R * R) != hipSuccess ||
+        hipMalloc(&sv, sizeof(double) * R) != hipSuccess ||
+        hipMalloc(&e, sizeof(double) * R) != hipSuccess ||
+        hipMalloc(&c, sizeof(double) * m * k) != hipSuccess ||
+        hipMalloc(&sgn, sizeof(double) * k) != hipSuccess ||
+        hipMalloc(&info, sizeof(rocblas_int)) != hipSuccess) {
+        cleanup();
+        snprintf(msg, msglen, "rsvd: hipMalloc failed");
+        return -5;
+    }
+    if (rocblas_create_handle(&h) != rocblas_status_success) {
+        cleanup();
+        return err("rocblas_create_handle", 0);
+    }
+    rocblas_set_stream(h, st);
+    int rc = 0;
+    if ((rc = launch_basis_transpose(d_s, a, m, ns, st))) {
+        cleanup();
+        return err("transpose", rc);
+    }
+    const double one = 1.0, zero = 0.0;
+    rocblas_status s;
+#define RS(call, what)                 \
+    if ((s = (call)) != rocblas_status_success) { \
+        cleanup();                     \
+        return err(what, (int)s);      \
+    }
+    // Y = S Omega
+    RS(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, M, R, NS, &one, a, M,
+                     d_omega, NS, &zero, y, M), "dgemm S.Omega");
+    for (int it = 0; it < n_iter; ++it) {
+        RS(rocsolver_dgeqrf(h, M, R, y, M, tau), "dgeqrf Y");
+        RS(rocsolver_dorgqr(h, M, R, R, y, M, tau), "dorgqr Y");
+        RS(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, NS, R, M, &one, a,
+                         M, y, M, &zero, z, NS), "dgemm S^T.Q");
+        RS(rocsolver_dgeqrf(h, NS, R, z, NS, tau), "dgeqrf Z");
+        RS(rocsolver_dorgqr(h, NS, R, R, z, NS, tau), "dorgqr Z");
+        RS(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, M, R, NS, &one, a, M,
+                         z, NS, &zero, y, M), "dgemm S.Z");
+    }
+    RS(rocsolver_dgeqrf(h, M, R, y, M, tau), "dgeqrf Q");
+    RS(rocsolver_dorgqr(h, M, R, R, y, M, tau), "dorgqr Q");
+    // B = Q^T S (R x ns), its SVD, U = Q U_B[:, :k]
+    RS(rocblas_dgemm(h, rocblas_operation_transpose, rocblas_operation_none, R, NS, M, &one, y, M,
+                     a, M, &zero, b, R), "dgemm Q^T.S");
+    RS(rocsolver_dgesvd(h, rocblas_svect_singular, rocblas_svect_none, R, NS, b, R, sv, ub, R,
+                        nullptr, 1, e, rocblas_outofplace, info), "dgesvd B");
+    RS(rocblas_dgemm(h, rocblas_operation_none, rocblas_operation_none, M, k, R, &one, y, M, ub, R,
+                     &zero, c, M), "dgemm Q.U_B");
+#undef RS
+    hipLaunchKernelGGL(col_sign_kernel, dim3(k), dim3(kPB), 0, st, c, m, sgn);
+    hipLaunchKernelGGL(col_scale_kernel, dim3(blocks(m * k)), dim3(kPB), 0, st, c, m, k,
+                       (const double *)sgn);
+    if ((rc = launch_basis_transpose(c, d_u, (size_t)k, (int)m, st))) {
+        cleanup();
+        return err("transpose back", rc);
+    }
+    (void)hipMemcpyAsync(d_sigma, sv, sizeof(double) * k, hipMemcpyDeviceToDevice, st);
+    rocblas_int hinfo = 0;
+    (void)hipMemcpyAsync(&hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return err("rsvd stream", 0);
+    }
+    cleanup();
+    if (hinfo != 0) {
+        snprintf(msg, msglen, "rocsolver_dgesvd did not converge (info=%d)", (int)hinfo);
+        return -6;
+    }
+    return 0;
+}
+
 }  // namespace burg

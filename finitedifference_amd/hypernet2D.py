@@ -243,17 +243,21 @@ def inviscid_burgers_implicit2D_LSPG(grid_x, grid_y, w0, dt, num_steps, mu, basi
 
 
 def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, return_ms=False):
-    """POD of a snapshot matrix (C/hypernet2D.py:2670-2695) on the GPU
-    (burg_pod: Householder QR of the tall matrix, SVD of R, Q applied to the
-    R-factor's singular vectors -- rocSOLVER, backward stable like LAPACK).
-    Returns (u, s) as the reference: method 'svd' -> all min(m, ns) modes
-    (np.linalg.svd(snaps, full_matrices=False), num_modes unused as there);
-    method 'rsvd' -> num_modes modes (default all).  'rsvd' returns the EXACT
-    truncated SVD that sklearn's randomized_svd approximates (the reference
-    calls it unseeded, so it has no reproducible output to match);
-    random_state is accepted and ignored.  Column signs follow sklearn's
-    svd_flip rule on u (largest-magnitude entry positive); np.linalg.svd's are
-    arbitrary."""
+    """POD of a snapshot matrix (C/hypernet2D.py:2670-2695) on the GPU.
+    Returns (u, s) as the reference:
+      method 'svd'  -> all min(m, ns) modes of the exact thin SVD
+                       (np.linalg.svd(snaps, full_matrices=False); num_modes
+                       unused, as there): burg_pod, rocSOLVER Householder QR of
+                       the tall matrix + SVD of R (backward stable like LAPACK);
+      method 'rsvd' -> num_modes modes (default all) by sklearn's
+                       randomized_svd algorithm (10 oversamples, n_iter 7 if
+                       num_modes < 0.1 min(m, ns) else 4, Gaussian test matrix
+                       drawn from check_random_state(random_state) exactly as
+                       sklearn draws it): burg_pod_rsvd, rocBLAS dgemm + QR on
+                       the device.  The power iterations are normalised by QR
+                       (sklearn's 'auto' uses LU: same subspace).
+    Column signs follow sklearn's svd_flip rule on u (largest-magnitude entry
+    positive); np.linalg.svd's are arbitrary."""
     if method not in ("svd", "rsvd"):
         raise ValueError("Unknown method '{}' for POD. Use 'svd' or 'rsvd'.".format(method))
     from . import _lib
@@ -268,8 +272,23 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
     sv = np.zeros(k)
     ms = ctypes.c_double(0.0)
     L = _lib.load()
-    _lib.check(L.burg_pod(int(device), m, ns, _lib.dptr(S), k, _lib.dptr(u), _lib.dptr(sv),
-                          ctypes.byref(ms)))
+    if method == "svd":
+        _lib.check(L.burg_pod(int(device), m, ns, _lib.dptr(S), k, _lib.dptr(u), _lib.dptr(sv),
+                              ctypes.byref(ms)))
+    else:
+        if random_state is None:
+            rng = np.random.mtrand._rand
+        elif isinstance(random_state, (int, np.integer)):
+            rng = np.random.RandomState(random_state)
+        else:
+            rng = random_state
+        nrand = min(k + 10, ns)
+        n_iter = 7 if k < 0.1 * min(m, ns) else 4
+        omega = rng.normal(size=(ns, nrand))
+        omega_cm = np.ascontiguousarray(omega.T)  # column-major (ns x nrand)
+        _lib.check(L.burg_pod_rsvd(int(device), m, ns, _lib.dptr(S), k, nrand, n_iter,
+                                   _lib.dptr(omega_cm), _lib.dptr(u), _lib.dptr(sv),
+                                   ctypes.byref(ms)))
     return (u, sv, ms.value) if return_ms else (u, sv)
 
 

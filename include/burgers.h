@@ -20,7 +20,8 @@
  *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
  *   burg_lspg           C/hypernet2D.py:133-200   inviscid_burgers_implicit2D_LSPG
  *                       with C/hypernet2D.py:1859-1929 gauss_newton_LSPG
- *   burg_pod            C/hypernet2D.py:2670-2695   POD (np.linalg.svd / randomized_svd)
+ *   burg_pod            C/hypernet2D.py:2670-2695   POD(method='svd') (np.linalg.svd)
+ *   burg_pod_rsvd       C/hypernet2D.py:2688-2692   POD(method='rsvd') (randomized_svd)
  *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
  *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
  *
@@ -260,6 +261,15 @@ int burg_lspg(burg_ctx *ctx, const double *w0, int num_steps, int n_pod, const d
  * of the factorisation (HIP events).  No context: runs on `device`. */
 int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *U, double *sigma,
              double *ms);
+
+/* Randomized truncated SVD, the algorithm of sklearn's randomized_svd that
+ * POD(method='rsvd') calls (C/hypernet2D.py:2688-2692): Y = S omega, n_iter
+ * power iterations (Householder-QR normalised), Q = orth(Y), SVD of Q^T S.
+ * omega: (ns x nrand) COLUMN-major host matrix (the caller's Gaussian draw,
+ * nrand = k + oversamples, k <= nrand <= ns); other arguments as burg_pod.
+ * All products are rocBLAS dgemm on the device. */
+int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
+                  const double *omega, double *U, double *sigma, double *ms);
 
 #ifdef __cplusplus
 }

@@ -630,7 +630,7 @@ def test_pod_vs_reference_and_oracle(gpu, orc, tag):
     assert rel(u @ (u.T @ S), S) < 1e-13
     uo, so = orc.pod_svd(S)
     assert np.max(np.abs(u[:, keep] - uo[:, keep])) < 1e-8
-    u10, s10 = H.POD(S, num_modes=10, method="rsvd")
+    u10, s10 = H.POD(S, num_modes=10, method="rsvd", random_state=0)
     assert u10.shape == (S.shape[0], 10)
     assert np.allclose(s10, g[f"{tag}_sr"], rtol=1e-8, atol=0)
     assert np.all(np.abs(np.sum(u10 * g[f"{tag}_ur"], axis=0)) > 1 - 1e-8)
@@ -644,11 +644,15 @@ def test_pod_tall_ragged_and_errors(gpu):
     rng = np.random.default_rng(11)
     m, ns = 2 * 37 * 37, 45
     S = rng.standard_normal((m, 8)) @ rng.standard_normal((8, ns)) + 1e-3 * rng.standard_normal((m, ns))
-    u, s = H.POD(S, num_modes=20, method="rsvd")
+    u, s = H.POD(S, num_modes=20, method="svd")
     un, sn, _ = np.linalg.svd(S, full_matrices=False)
-    assert np.allclose(s, sn[:20], rtol=1e-12)
+    assert np.allclose(s, sn, rtol=1e-12)
+    u, s = u[:, :20], s[:20]
     keep = _pod_mode_mask(sn[:20], rel_floor=1e-12, rel_gap=1e-8)
     assert np.all(np.abs(np.sum(u[:, keep] * un[:, :20][:, keep], axis=0)) > 1 - 1e-9)
+    ur, sr = H.POD(S, num_modes=8, method="rsvd", random_state=3)  # the rank-8 part
+    assert np.allclose(sr, sn[:8], rtol=1e-10)
+    assert np.all(np.abs(np.sum(ur * un[:, :8], axis=0)) > 1 - 1e-10)
     with pytest.raises(ValueError):
         H.POD(S.T)
     L = _lib.load()

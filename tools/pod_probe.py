@@ -31,14 +31,22 @@ def main():
     del sn
     t_fom = time.time() - t
     H.POD(S[:, :64], method="svd")  # warm-up (rocBLAS/rocSOLVER init)
-    t = time.time()
-    u, s, ms = H.POD(S, num_modes=95, method="rsvd", return_ms=True)
-    t_pod = time.time() - t
+    H.POD(S[:, :64], num_modes=8, method="rsvd", random_state=0)
     m, ns = S.shape
-    print(json.dumps({"N": N, "T": T, "nmu": nmu, "shape": [m, ns], "fom_sweep_s": t_fom,
-                      "pod_wall_s": t_pod, "pod_device_ms": ms,
-                      "qr_tflops_equiv": 2.0 * m * ns * ns / (ms / 1e3) / 1e12,
-                      "s0": float(s[0]), "s94_rel": float(s[94] / s[0])}))
+    out = {"N": N, "T": T, "nmu": nmu, "shape": [m, ns], "fom_sweep_s": t_fom}
+    t = time.time()
+    u, s, ms = H.POD(S, num_modes=95, method="rsvd", random_state=0, return_ms=True)
+    r = 105
+    flops = 2.0 * m * ns * r * (2 + 2 * 7) + 2.0 * m * ns * r  # S.Omega, 7 x (S^T.Q, S.Z), Q^T.S
+    out["rsvd"] = {"wall_s": time.time() - t, "device_ms": ms, "gemm_flops": flops,
+                   "gemm_TFLOPs_equiv": flops / (ms / 1e3) / 1e12,
+                   "s0": float(s[0]), "s94_rel": float(s[94] / s[0])}
+    t = time.time()
+    ue, se, mse = H.POD(S, method="svd", return_ms=True)
+    out["svd"] = {"wall_s": time.time() - t, "device_ms": mse,
+                  "rsvd_vs_exact_s_maxrel": float(np.max(np.abs(s / se[:95] - 1))),
+                  "rsvd_vs_exact_min_abs_cos_top50": float(np.min(np.abs(np.sum(u[:, :50] * ue[:, :50], axis=0))))}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
