@@ -195,6 +195,9 @@ int launch_lspg_project(const double *bt, const double *x, int npod, size_t m, d
 int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t st);
 int launch_lspg_solve(const double *G, int npod, double *y, double *dy, unsigned *err,
                       hipStream_t st);
+// the same with rocSOLVER potrf/potrs (handle: a rocblas_handle on st)
+int launch_lspg_solve_lib(void *handle, double *G, int npod, double *d0, int *info, double *y,
+                          unsigned *err, hipStream_t st);
 // POD (pod.hip): exact thin SVD of a C-order (m x ns) device matrix via
 // rocSOLVER QR + SVD of R; U (m x k, C-order) and the k leading singular values
 int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, double *d_u,

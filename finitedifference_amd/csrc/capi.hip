@@ -2,6 +2,7 @@
 // time loop (inviscid_burgers_implicit2D, C/hypernet2D.py:72-131) and the
 // parity hooks.  Host-side only; kernels live in march.hip / stencil.hip.
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1578,10 +1579,19 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
            *d_wp = nullptr, *d_y = nullptr, *d_part = nullptr, *d_G = nullptr, *d_chunk = nullptr,
            *d_tr = nullptr;
     unsigned *d_err = nullptr;
+    int *d_info = nullptr;
+    double *d_d0 = nullptr;
+    rocblas_handle rh = nullptr;
+    // solver of the npod x npod normal equations: our one-workgroup kernel or
+    // rocSOLVER potrf/potrs (BURG_LSPG_SOLVE=kernel|lib)
+    const char *solve_env = getenv("BURG_LSPG_SOLVE");
+    const bool lib_solve = !(solve_env && std::strcmp(solve_env, "kernel") == 0);
     bool registered = false;
     std::vector<hipEvent_t> evs;
     auto cleanup = [&]() {
         (void)hipStreamSynchronize(c->stream);
+        if (rh) rocblas_destroy_handle(rh);
+        dfree(d_info), dfree(d_d0);
         if (registered) (void)hipHostUnregister(snaps);
         for (auto e : evs) (void)hipEventDestroy(e);
         dfree(d_b), dfree(d_bt), dfree(d_btT), dfree(d_w), dfree(d_wT), dfree(d_wp), dfree(d_y);
@@ -1631,6 +1641,16 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     LCHK(dalloc(&d_G, (size_t)P * P));
     LCHK(dalloc(&d_err, 1));
     LHIP(hipMemsetAsync(d_err, 0, sizeof(unsigned), c->stream));
+    if (lib_solve) {
+        LCHK(dalloc(&d_info, 1));
+        LCHK(dalloc(&d_d0, (size_t)P));
+        if (rocblas_create_handle(&rh) != rocblas_status_success) {
+            rc = fail(BURG_EHIP, "burg_lspg: rocblas_create_handle failed");
+            cleanup();
+            return rc;
+        }
+        rocblas_set_stream(rh, c->stream);
+    }
 
     // kept snapshots: S states at a time, transposed into the C-order columns
     int S = 0;
@@ -1734,7 +1754,10 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
             LHIP(hipEventRecord(evs[0], c->stream));
             LLAUNCH(launch_lspg_gram(la, d_part, d_G, c->stream));
             LHIP(hipEventRecord(evs[1], c->stream));
-            LLAUNCH(launch_lspg_solve(d_G, n_pod, d_y, nullptr, d_err, c->stream));
+            if (lib_solve)
+                LLAUNCH(launch_lspg_solve_lib(rh, d_G, n_pod, d_d0, d_info, d_y, d_err, c->stream));
+            else
+                LLAUNCH(launch_lspg_solve(d_G, n_pod, d_y, nullptr, d_err, c->stream));
             LCHK(expand());
             LHIP(hipEventRecord(evs[4], c->stream));
             LHIP(hipEventSynchronize(evs[4]));

@@ -25,6 +25,8 @@
 #include "burg_internal.h"
 
 #include <hip/hip_runtime.h>
+#include <rocblas/rocblas.h>
+#include <rocsolver/rocsolver.h>
 
 namespace burg {
 namespace {
@@ -384,6 +386,28 @@ __global__ __launch_bounds__(kLB) void lspg_solve_kernel(const double *__restric
     if (tid == 0 && bad) *err = 1u;
 }
 
+// library solve (rocSOLVER potrf/potrs on G in place): the diagonal before
+// the factorisation, then the rank check and y += dy (dy = G[npod*P..])
+__global__ __launch_bounds__(kLB) void lspg_diag_kernel(const double *__restrict__ G, int P,
+                                                        int npod, double *__restrict__ d0)
+{
+    const int k = blockIdx.x * kLB + threadIdx.x;
+    if (k < npod) d0[k] = G[(size_t)k * P + k];
+}
+
+__global__ __launch_bounds__(kLB) void lspg_finish_kernel(const double *__restrict__ G, int P,
+                                                          int npod, const double *__restrict__ d0,
+                                                          const int *__restrict__ info,
+                                                          double *__restrict__ y,
+                                                          unsigned *__restrict__ err)
+{
+    const int k = blockIdx.x * kLB + threadIdx.x;
+    if (k >= npod) return;
+    const double l = G[(size_t)k * P + k];
+    if (*info != 0 || !(l * l > 0x1p-49 * d0[k])) *err = 1u;
+    y[k] += G[(size_t)npod * P + k];
+}
+
 constexpr int kMfmaGroups = 512;  // 2 per CU (57 KB of LDS each at P = 96)
 constexpr int kSumSlices = 16;
 
@@ -450,6 +474,23 @@ int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t 
                        (const double *)partial, ng, (size_t)PP, PP, mid);
     hipLaunchKernelGGL(lspg_sum_kernel, dim3((PP + kLB - 1) / kLB, 1), dim3(kLB), 0, st,
                        (const double *)mid, kSumSlices, (size_t)PP, PP, G);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_lspg_solve_lib(void *handle, double *G, int npod, double *d0, int *info, double *y,
+                          unsigned *err, hipStream_t st)
+{
+    // G is symmetric: its row-major (P x P) storage is the column-major one
+    rocblas_handle h = (rocblas_handle)handle;
+    const int P = lspg_cols(npod);
+    hipLaunchKernelGGL(lspg_diag_kernel, dim3(1), dim3(kLB), 0, st, (const double *)G, P, npod, d0);
+    if (rocsolver_dpotrf(h, rocblas_fill_lower, npod, G, P, info) != rocblas_status_success)
+        return -3;
+    if (rocsolver_dpotrs(h, rocblas_fill_lower, npod, 1, G, P, G + (size_t)npod * P, npod) !=
+        rocblas_status_success)
+        return -3;
+    hipLaunchKernelGGL(lspg_finish_kernel, dim3(1), dim3(kLB), 0, st, (const double *)G, P, npod,
+                       (const double *)d0, (const int *)info, y, err);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
