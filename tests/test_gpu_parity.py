@@ -660,3 +660,26 @@ def test_pod_tall_ragged_and_errors(gpu):
     sv = np.zeros(1)
     assert L.burg_pod(0, m, ns, _lib.dptr(np.ascontiguousarray(S)), 0, _lib.dptr(out),
                       _lib.dptr(sv), None) == _lib.BURG_EINVAL
+
+
+def test_lspg_solve_kernel_path(gpu, monkeypatch):
+    """BURG_LSPG_SOLVE=kernel selects the one-workgroup Cholesky kernel instead
+    of rocSOLVER potrf/potrs: same Gauss-Newton counts and trajectory (within
+    round-off) on the reference's n24 case, and the rank check still fires."""
+    from finitedifference_amd import _lib
+    from finitedifference_amd import hypernet2D as H
+    g = golden("ref_lspg.npz")
+    N, T, m1, m2, dt, npod = g["n24_meta"]
+    N, T = int(N), int(T)
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    B = g["n24_basis"]
+    a, (na, *_) = H.inviscid_burgers_implicit2D_LSPG(gx, gy, np.ones(2 * N * N), dt, T, (m1, m2), B,
+                                                     verbose=False)
+    monkeypatch.setenv("BURG_LSPG_SOLVE", "kernel")
+    b, (nb, *_) = H.inviscid_burgers_implicit2D_LSPG(gx, gy, np.ones(2 * N * N), dt, T, (m1, m2), B,
+                                                     verbose=False)
+    assert na == nb == int(g["n24_its"].sum())
+    assert rel(b, a) <= 1e-13 and rel(b, g["n24_snaps"]) <= REF_TOL
+    with pytest.raises(_lib.BurgersError):
+        H.inviscid_burgers_implicit2D_LSPG(gx, gy, np.ones(2 * N * N), dt, 1, (m1, m2),
+                                           np.hstack([B[:, :3], B[:, :1]]), verbose=False)
