@@ -27,7 +27,8 @@ SURVEY.md section 8(d); per-launch device time from HIP events on the
 library's stream; peak 8 TB/s; traffic from the committed rocprofv3 PMC
 passes, profiles/pmc_traffic.json) and cpu_baseline (the oracle's CPU
 restatement of the reference Newton algorithm, rank 0 at N = 1, bounded
-sample).  Only the cpu_baseline leg touches oracle/.
+sample).  Only the cpu_baseline leg touches oracle/.  rom_pipeline: secondary
+numbers of the reference's ROM driver at 250^2 (sweep, POD, LSPG; --no-rom skips).
 """
 import argparse
 import json
@@ -63,6 +64,8 @@ def parse():
     ap.add_argument("--stream-w", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rom", action="store_true",
+                    help="skip the secondary ROM-pipeline numbers (sweep, POD, LSPG at 250^2)")
     ap.add_argument("--stencil-nx", type=int, default=8192,
                     help="grid of the residual / J.x roofline probe (0: skip)")
     ap.add_argument("--rehearse-one-gpu", action="store_true",
@@ -124,6 +127,49 @@ def stencil_roofline(nx, reps=20, pmc_file=None):
                   "traffic": traffic, "traffic_source": tsrc}
     ctx.close()
     return out
+
+
+ROM_MUS = [(4.25, 0.015), (4.25, 0.0225), (4.25, 0.03), (4.875, 0.015), (4.875, 0.0225),
+           (4.875, 0.03), (5.5, 0.015), (5.5, 0.0225), (5.5, 0.03)]
+
+
+def rom_pipeline(N=250, T=500, npod=95, rom_steps=20):
+    """The reference's ROM driver (C/run_prom.py:24-110) on the GPU at its own
+    size (250^2, 9 training mu x 500 steps, 95 POD modes): the FOM snapshot
+    sweep, POD (rsvd), and LSPG PROM steps at the out-of-sample mu
+    (4.75, 0.02).  Secondary numbers -- not the headline metric.  The LSPG
+    fused J.basis + Gram kernel's achieved rate is on its algorithmic bytes
+    (DESIGN.md section 4.6)."""
+    from finitedifference_amd import hypernet2D as H
+    from finitedifference_amd.solver import FOMContext
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    m = 2 * N * N
+    t0 = time.perf_counter()
+    sn = H.inviscid_burgers_implicit2D_sweep(gx, gy, np.ones(m), DT, T, ROM_MUS, verbose=0)
+    t_sweep = time.perf_counter() - t0
+    S = np.hstack(sn)
+    del sn
+    u, s, pod_ms = H.POD(S, num_modes=npod, method="rsvd", random_state=0, return_ms=True)
+    del S
+    ctx = FOMContext(N, N)
+    ctx.set_problem(gx, gy, DT, (4.75, 0.02))
+    ctx.lspg(np.ones(m), 1, u, keep_snaps=False)  # warm-up
+    _, _, its, _, times, st = ctx.lspg(np.ones(m), rom_steps, u, keep_snaps=False)
+    ctx.close()
+    upd = max(st["newton_updates"], 1)
+    gram_ms = times[0] / upd
+    alg = 2 * m * npod * 8 + 4 * m * 8
+    return {"grid": f"{N}x{N}", "training": f"{len(ROM_MUS)} mu x {T} steps", "npod": npod,
+            "fom_sweep_s_incl_d2h": round(t_sweep, 3), "pod_rsvd_device_ms": round(pod_ms, 2),
+            "lspg_ms_per_step": round(st["loop_ms"] / rom_steps, 4),
+            "lspg_gn_norms_per_step": float(its.mean()),
+            "lspg_gram": {"avg_launch_ms": round(gram_ms, 4), "alg_bytes": alg,
+                          "achieved": round(alg / gram_ms / 1e6, 1), "unit": "GB/s",
+                          "frac": round(alg / gram_ms / 1e6 / HBM_PEAK_GBS, 4)},
+            "reference_cpu_1core_build_container": {
+                "lspg_s_per_step": 1.03, "pod_rsvd_s": 49.6,
+                "source": "profiles/r01/lspg/reference_cpu_timing.txt, "
+                          "profiles/r01/pod/reference_cpu_timing.txt"}}
 
 
 def read_pmc(path, key):
@@ -258,6 +304,8 @@ def main():
         }
         if world == 1 and args.stencil_nx > 0:
             out["stencil_roofline"] = stencil_roofline(args.stencil_nx, pmc_file=args.pmc_file)
+        if world == 1 and not args.no_rom:
+            out["rom_pipeline"] = rom_pipeline()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(nx, args.cpu_seconds)
         print(json.dumps(out), flush=True)
