@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -58,6 +58,7 @@ class BurgStats(ctypes.Structure):
         ("slow_ticks", ctypes.c_int64),
         ("ieee_diagonals", ctypes.c_int64),
         ("comm_polls", ctypes.c_int64),
+        ("nonfinite_diagonals", ctypes.c_int64),
     ]
 
     def as_dict(self):

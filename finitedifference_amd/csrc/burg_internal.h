@@ -72,6 +72,7 @@ struct StreamStats {
     unsigned long long why[6];          // slow-path causes: 0 east slot busy, 1 north slot
                                         // busy, 2 west not written, 3 south not written,
                                         // 4 range (IEEE redo), 5 entries that needed a re-poll
+    unsigned long long nonfinite_diagonals;  // diagonals whose new state has a NaN / Inf
 };
 
 // Tiling of a slab for the streaming engine: nti strips of 64 rows, ntj tiles
@@ -133,7 +134,9 @@ struct PipeArgs {
     int qbase;            // absolute step of local step 0, mod 2*kPipeR (sentinel colour)
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
-    unsigned *err;        // [4]: flag, tile, diagonal/step, which wait
+    long long census_ticks;  // how long the residency census may wait for the whole grid
+    unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)
+    unsigned *census;     // workgroups checked in (zeroed before every launch)
     StreamStats *stats;
 };
 
@@ -168,6 +171,7 @@ int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
                         int ldo, hipStream_t st);
 bool pipe_width_supported(int W);
+bool pipe_sweep_width_supported(int W);
 int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);

@@ -127,6 +127,10 @@ struct burg_ctx {
     int sw_T = 0;
     const d2 *sw_colc = nullptr;
     const double *sw_lbc = nullptr;
+    // one-trajectory override of the column table / inlet terms (wide-tile
+    // sweeps run one launch per mu)
+    const d2 *ov_colc = nullptr;
+    const double *ov_lbc = nullptr;
     long long spin_ticks = 500000000LL;  // 5 s of s_memrealtime (100 MHz)
     // multi-GPU halo rings (pinned shared host memory)
     std::string halo_name;
@@ -316,32 +320,44 @@ void stream_free(burg_ctx *c)
     c->sp_ready = c->colc_ready = false;
 }
 
-// Pipe engine plan: W in {8, 16} (the narrowest whose tile count fits the
-// target), every workgroup (4 tiles + comm wave) resident at once.
+// Pipe engine plan: the narrowest W in {8, 16, ..., 1024} whose tile count
+// fits the target (1024 = one compute wave per SIMD), every workgroup (4
+// tiles + comm wave) resident at once; W <= 16 keeps the previous states in
+// LDS, wider tiles stream them from the HBM ring (pipe.hip).
 bool pipe_plan(burg_ctx *c, int target, StreamPlan *out, int *nwj)
 {
-    int Ws[2] = {8, 16};
-    int n = 2;
+    std::vector<int> Ws;
     if (c->stream_w_opt != 0) {
         if (!pipe_width_supported(c->stream_w_opt)) return false;
-        Ws[0] = c->stream_w_opt;
-        n = 1;
+        Ws.push_back(c->stream_w_opt);
+    } else {
+        for (int W = 8; W <= 1024; W *= 2) Ws.push_back(W);
     }
-    for (int i = 0; i < n; ++i) {
-        const int W = Ws[i];
+    int fit = -1;
+    StreamPlan pf{};
+    int wf = 0;
+    for (int W : Ws) {
         StreamPlan p = plan_stream(c->nx, c->nrows, 0, W);
         const int wj = (p.ntj + 3) / 4;
         const int cap = pipe_max_resident_blocks(W);
         if (cap < 0) return false;
-        const bool last = i + 1 == n;
-        if (p.nti * wj <= cap && (p.ntiles <= target || last)) {
-            p.R = kPipeR;
+        if (p.nti * wj > cap) continue;
+        p.R = kPipeR;
+        if (fit < 0) {
+            fit = W;
+            pf = p;
+            wf = wj;
+        }
+        if (p.ntiles <= target) {
             *out = p;
             *nwj = wj;
             return true;
         }
     }
-    return false;
+    if (fit < 0) return false;
+    *out = pf;
+    *nwj = wf;
+    return true;
 }
 
 // Plan the tiling (capped by residency: every tile's wavefront must be live
@@ -361,7 +377,7 @@ int stream_setup(burg_ctx *c)
                 return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB");
             if (int e = dalloc(&c->d_boxes, c->box16)) return e;
             if (int e = dalloc(&c->d_colc, (size_t)pp.ntj * pp.W)) return e;
-            if (int e = dalloc(&c->d_err, 4)) return e;
+            if (int e = dalloc(&c->d_err, 8)) return e;
             if (int e = dalloc(&c->d_sstats, 1)) return e;
             CHK(launch_pipe_fill(c->d_boxes, c->box16, 0, c->stream));
             HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
@@ -372,7 +388,7 @@ int stream_setup(burg_ctx *c)
             if (c->world > 1)
                 return fail(BURG_ESHAPE,
                             "multi-GPU slabs need the pipe engine: a %d-row x %d slab does not fit "
-                            "one resident workgroup per 4 tiles of width 8 or 16",
+                            "one resident workgroup per 4 tiles of width <= 1024",
                             c->nrows, c->nx);
             StreamPlan p = plan_stream(c->nx, c->nrows, target,
                                        c->engine == BURG_ENGINE_PIPE ? 0 : c->stream_w_opt);
@@ -397,7 +413,7 @@ int stream_setup(burg_ctx *c)
                             p.ntiles, p.W);
             if (int e = dalloc(&c->d_boxes, c->box16)) return e;
             if (int e = dalloc(&c->d_colc, (size_t)p.ntj * p.W)) return e;
-            if (int e = dalloc(&c->d_err, 4)) return e;
+            if (int e = dalloc(&c->d_err, 8)) return e;
             if (int e = dalloc(&c->d_sstats, 1)) return e;
             CHK(launch_fill_sentinel(c->d_boxes, c->box16, c->stream));
             HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
@@ -448,8 +464,9 @@ StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
     return a;
 }
 
-// max steps per launch so that K*W stays an int
-int stream_max_steps(const burg_ctx *c) { return (1 << 29) / c->sp.W; }
+// max steps per launch: a tile's ring (L = K*W + W + 96 entries of 1 KB) must
+// stay addressable by one buffer descriptor (< 2 GiB)
+int stream_max_steps(const burg_ctx *c) { return ((1 << 21) - 4096) / c->sp.W - 1; }
 
 PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
 {
@@ -476,8 +493,12 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.ntiles = c->sp.ntiles;
     a.nwj = c->nwj;
     a.spin_ticks = c->spin_ticks;
+    a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
     a.err = c->d_err;
+    a.census = c->d_err + 4;
     a.stats = c->d_sstats;
+    if (c->ov_colc) a.colc = c->ov_colc;
+    if (c->ov_lbc) a.cf.lbc = c->ov_lbc;
     return a;
 }
 
@@ -507,6 +528,12 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
             (void)launch_fill_sentinel(c->d_boxes, c->box16, c->stream);
         }
         (void)hipStreamSynchronize(c->stream);
+        if (pipe && err[3] == 64u)
+            return fail(BURG_EHIP,
+                        "pipe engine: only %u of %d workgroups became resident together (W=%d); "
+                        "the pipeline needs the whole grid on the GPU at once -- another kernel "
+                        "or process holds CUs",
+                        err[2], c->sp.nti * c->nwj, c->sp.W);
         if (pipe)
             return fail(BURG_EHIP,
                         "pipe engine: a wait timed out (workgroup tile %u of %d, step/diagonal %u, "
@@ -554,7 +581,13 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->stream_launches = launches;
         st->ieee_diagonals = (int64_t)ss.ieee_diagonals;
         st->comm_polls = c->eng_eff == BURG_ENGINE_PIPE ? (int64_t)ss.why[5] : 0;
+        st->nonfinite_diagonals = (int64_t)ss.nonfinite_diagonals;
     }
+    if (ss.nonfinite_diagonals)
+        return fail(BURG_ENAN,
+                    "the march produced non-finite states (NaN/Inf) on %llu diagonals: a NaN/Inf "
+                    "input or a negative discriminant 0.25 + hx*Cu + hy*Cv",
+                    (unsigned long long)ss.nonfinite_diagonals);
     return 0;
 }
 
@@ -600,31 +633,56 @@ int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
 // One device-resident trajectory: num_steps steps from d_state[cur] in ONE
 // launch, every state kept in the ring (HBM) -- the reference's snapshot
 // matrix in ring layout (C/hypernet2D.py:89-126 keeps them all); the final
-// state becomes d_state[cur].
+// state becomes d_state[cur].  A trajectory whose ring does not fit in 85 % of
+// free HBM (or one descriptor) runs as several launches over a ring of C
+// steps, each launch continuing from the previous one's last states.
 int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats *st)
 {
     if (int e = stream_setup(c)) return e;
     if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
-    if (num_steps > stream_max_steps(c))
-        return fail(BURG_EINVAL, "num_steps %d exceeds one launch (%d)", num_steps,
-                    stream_max_steps(c));
     const int W = c->sp.W;
-    const long long L = (long long)num_steps * W + W + 96;
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    long long C = std::min(num_steps, stream_max_steps(c));
+    if ((size_t)(C * W + W + 96) * per_entry > c->ring_entries * sizeof(d2)) {
+        // need a (bigger) ring: size it against free memory
+        dfree(c->d_ring);
+        c->ring_entries = 0;
+        size_t freeb = 0, totalb = 0;
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        const long long Lmax = (long long)(freeb / 100 * 85 / per_entry);
+        C = std::min<long long>(C, (Lmax - W - 96) / W);
+        if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
+    } else {
+        C = std::min<long long>(C, ((long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave)) -
+                                    W - 96) / W);
+    }
+    const long long L = C * W + W + 96;
     if (int e = ensure_ring(c, L)) return e;
     if (from_initial && !c->d_w0) return fail(BURG_ESTATE, "no uploaded initial state");
     stream_stats_begin(c);
     CHK(launch_ring_load(stream_args(c, L, 0, 0), W, from_initial ? c->d_w0 : c->d_state[c->cur],
                          c->stream));
     float ms = 0.f;
-    if (int e = stream_launch(c, L, 0, num_steps, &ms)) return e;
-    CHK(launch_ring_extract(stream_args(c, L, 0, 0), W, num_steps, 1, 1, c->d_state[c->cur ^ 1],
+    long long origin = 0;
+    int done = 0, last = 0;
+    int64_t launches = 0;
+    while (done < num_steps) {
+        const int K = (int)std::min<long long>(num_steps - done, C);
+        if (int e = stream_launch(c, L, origin, K, &ms)) return e;
+        origin = (origin + (long long)K * W) % L;
+        done += K;
+        last = K;
+        ++launches;
+    }
+    const long long o_last = ((origin - (long long)last * W) % L + L) % L;
+    CHK(launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1, c->d_state[c->cur ^ 1],
                             1, c->stream));
     c->cur ^= 1;
-    if (int e = stream_stats_end(c, st, num_steps, 1)) return e;
+    if (int e = stream_stats_end(c, st, num_steps, launches)) return e;
     if (st) {
         st->loop_ms = ms;
         st->march_kernel_ms = ms;
-        st->march_launches = 1;
+        st->march_launches = launches;
     }
     return 0;
 }
@@ -1184,7 +1242,10 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
     if (c->eng_eff != BURG_ENGINE_PIPE)
         return fail(BURG_ESHAPE, "burg_sweep runs on the pipe engine; this %d x %d grid needs "
                     "the streaming engine's wider tiles", c->nx, c->nrows);
-    {
+    // narrow tiles run a group of trajectories per launch (the sweep kernel);
+    // wide tiles one launch per trajectory with that mu's coefficient tables
+    const bool narrow = pipe_sweep_width_supported(c->sp.W);
+    if (narrow) {
         const int cap = pipe_max_resident_blocks(c->sp.W, true);
         if (cap < c->sp.nti * c->nwj)
             return fail(BURG_ESHAPE, "burg_sweep: %d workgroups of the sweep kernel cannot all be "
@@ -1201,6 +1262,8 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
         c->sw_T = 0;
         c->sw_colc = nullptr;
         c->sw_lbc = nullptr;
+        c->ov_colc = nullptr;
+        c->ov_lbc = nullptr;
         (void)hipStreamSynchronize(c->stream);
         if (registered)
             for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(snaps[j]);
@@ -1230,7 +1293,7 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
     long long G = (Lmax - W - 96) / ((long long)T * W);
     G = std::min<long long>(G, nmu);
     G = std::min<long long>(G, stream_max_steps(c) / T);
-    G = std::min<long long>(G, kPipeSweepMax);
+    G = std::min<long long>(G, narrow ? kPipeSweepMax : 1);
     if (const char *e = std::getenv("BURG_SWEEP_GROUP")) {  // test knob: force grouping
         const long long v = std::atoll(e);
         if (v > 0) G = std::min(G, v);
@@ -1273,11 +1336,18 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
     for (int g0 = 0; g0 < nmu && rc == BURG_OK; g0 += (int)G) {
         const int nb = (int)std::min<long long>(G, nmu - g0);
         if ((rc = launch_ring_load(stream_args(c, L, 0, 0), W, c->d_w0, c->stream))) break;
-        c->sw_T = T;
-        c->sw_colc = d_colcb + (size_t)g0 * ncolp;
-        c->sw_lbc = d_lbcb + (size_t)g0 * c->nrows;
+        if (narrow) {
+            c->sw_T = T;
+            c->sw_colc = d_colcb + (size_t)g0 * ncolp;
+            c->sw_lbc = d_lbcb + (size_t)g0 * c->nrows;
+        } else {
+            c->ov_colc = d_colcb + (size_t)g0 * ncolp;
+            c->ov_lbc = d_lbcb + (size_t)g0 * c->nrows;
+        }
         rc = stream_launch(c, L, 0, nb * T, &ms);
         c->sw_T = 0;
+        c->ov_colc = nullptr;
+        c->ov_lbc = nullptr;
         if (rc) break;
         ++launches;
         last_nb = nb;

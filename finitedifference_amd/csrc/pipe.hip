@@ -10,7 +10,7 @@
 // is lane r-1's north outflow of the previous diagonal (one DPP move) and the
 // west inflow is the lane's own east outflow, except at tile edges.
 //
-// What is new here is WHO moves the edge data and through what:
+// WHO moves the edge data, and through what:
 //   * a workgroup = 4 compute waves = 4 horizontally adjacent tiles of one
 //     strip, plus one comm wave (320 threads, one workgroup per CU);
 //   * west->east edges between the workgroup's own tiles go through LDS rings;
@@ -18,11 +18,26 @@
 //     deposits the granules into LDS inboxes, writes the global slot back to
 //     "empty", and grants the compute waves permission to overwrite their
 //     outbound global slots;
-//   * so the compute waves never load from global memory: they read LDS, run
-//     the cell chain and fire-and-forget their stores (trajectory ring and
-//     outbound granules).  A global load's wait would also wait for every
-//     older store of the wave (vmcnt counts both, in order) -- that coupling
-//     cost the streaming engine half its time (profiles/r01/README.md).
+//   * so the compute waves never wait on a global load of edge data: they read
+//     LDS, run the cell chain and fire-and-forget their stores (trajectory
+//     ring and outbound granules).
+//
+// Where the previous step of a cell comes from depends on the tile width:
+//   * narrow tiles (W = 8, 16): the lane's own output of diagonal s - W, kept
+//     in LDS (st[W][64]): no global load at all in the loop;
+//   * wide tiles (W = 32 .. 1024, the 4096^2 grid and the multi-GPU slabs of
+//     2048 x 8192 / 16384 cells): the tile's trajectory ring in HBM, entry
+//     s - W (written by the same wave W diagonals earlier: same-wave program
+//     order), prefetched kPf diagonals ahead into registers -- one coalesced
+//     1 KB load per diagonal.  Its s_waitcnt waits only for memory operations
+//     at least kPf diagonals old (vmcnt counts loads and stores in issue order).
+//
+// South/north streams are indexed by diagonal: comm lane j of wave k's group
+// of 16 handles the diagonals d = j (mod 16) of that tile -- the granule of
+// (step d / W, column d % W).  The comm wave polls a stream only when the
+// compute wave that needs it is at most kLA diagonals away (each compute wave
+// publishes its progress in LDS), so the mailboxes are not re-read thousands
+// of times before their data can exist.
 //
 // Global mailbox slots carry two sentinel colours: a slot is free for step q
 // when it holds the sentinel of q's colour ((q / kPipeR) & 1); the consumer,
@@ -31,12 +46,16 @@
 // the producer's own (possibly still in flight) store of step q - kPipeR.
 //
 // Multi-GPU: the bottom strip's south inflow and the top
-// strip's north outflow may live in pinned host memory shared with the
-// neighbour rank's process (halo_in / halo_out), accessed at system scope
-// (sc0 sc1); the protocol is unchanged.
+// strip's north outflow may live in memory shared with the neighbour rank's
+// process (halo_in / halo_out: pinned host memory or the consumer GPU's own
+// memory), accessed at system scope (sc0 sc1); the protocol is unchanged.
 //
-// Every wait is bounded in wall time (s_memrealtime): a wave that gives up
-// sets the error word and the LDS abort flag, and the launch drains.
+// Residency: the pipeline needs every workgroup on the GPU at once.  Before
+// its first wait each workgroup checks in on a census counter; if the whole
+// grid is not resident within a bounded time the launch fails fast
+// (err[3] = 64) instead of stalling.  Every later wait is bounded in wall time
+// (s_memrealtime): a wave that gives up sets the error word and the LDS abort
+// flag, and the launch drains.
 #include <climits>
 
 #include "burg_internal.h"
@@ -57,6 +76,10 @@ constexpr int kR = kPipeR;
 constexpr int kRL = kPipeRL;
 constexpr unsigned G = kGranuleStride;
 constexpr int kThreads = 5 * kWave;
+constexpr int kNI = 64;   // south inbox ring (diagonals), power of two
+constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
+constexpr int kLA = 16;   // poll window (diagonals ahead of a compute wave's progress)
+constexpr int kPf = 8;    // wide tiles: prefetch distance of the previous state (diagonals)
 
 __device__ __forceinline__ d2 as_d2(v4u v)
 {
@@ -120,7 +143,7 @@ __device__ __forceinline__ double shr1_or(double old0, double x)
 }
 
 // device mailboxes: sc1 (agent scope, write-through, L1 bypass);
-// host halo rings: sc0 sc1 (system scope)
+// halo rings shared with another process / GPU: sc0 sc1 (system scope)
 __device__ __forceinline__ v4u ld_dev(__amdgpu_buffer_rsrc_t rs, unsigned off)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16);
@@ -170,28 +193,38 @@ __device__ __forceinline__ void lds_sti(void *p, int v) { *(volatile lds_i32 *)p
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
 
+template <int W>
+constexpr bool is_wide() { return W > 16; }
+
 // LDS image of one workgroup (SWEEP: a parameter sweep, burg_sweep -- the
 // initial state and every trajectory's source / inlet terms stay on chip)
 template <int W, bool SWEEP>
 struct PipeLds {
+    static constexpr bool WIDE = is_wide<W>();
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
-    v4u st[4][W][kWave];    // per wave: the lane's outputs of the last W diagonals
+    v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
-    double srcb[kSW][4][W];                        // sweep: src of trajectory j, by column
+    double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
     double lbt[kSW][kWave];                        // sweep: inlet term of trajectory j, by row
     v4u cc[4][W];           // per wave: {hx, src} of the tile's columns
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
-    v4u ins[4][kRL][W];     // south inflow of each wave (comm wave deposits)
+    v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
-    int perm[8];            // [0..3] north grants per wave, [4] east grant of wave 3, [5] abort
+    int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
+                            // (step), [5] abort
+    int prog[4];            // per compute wave: first diagonal of its current block
 };
 
 template <int W, bool SWEEP>
 __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
 {
-    static_assert(W == 8 || W == 16, "pipe engine: W in {8, 16}");
+    constexpr bool WIDE = is_wide<W>();
+    static_assert(W == 8 || W == 16 || (WIDE && W <= 1024 && (W & (W - 1)) == 0),
+                  "pipe engine: W in {8, 16, 32, ..., 1024}");
+    static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
+    constexpr int U = WIDE ? kPf : 4;  // diagonals per block (progress published per block)
     __shared__ PipeLds<W, SWEEP> sm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -209,11 +242,45 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     const bool north_dev = ti + 1 < a.nti, north_host = ti + 1 == a.nti && a.halo_out != nullptr;
     const int hcols = a.cf.nx;  // halo ring row length (granules): real columns only
 
+    // ---- residency census: every workgroup must be on the GPU at once
+    if (threadIdx.x == 0) {
+        int ok = 1;
+        if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+            ok = 0;
+        } else {
+            atomicAdd(a.census, 1u);
+            const long long t0 = now_rt();
+            for (;;) {
+                const unsigned n = __hip_atomic_load(a.census, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                if (n >= gridDim.x) break;
+                if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                    ok = 0;
+                    break;
+                }
+                if (now_rt() - t0 > a.census_ticks) {
+                    if (atomicOr(a.err, 1u) == 0) {
+                        a.err[1] = (unsigned)wg;
+                        a.err[2] = n;
+                        a.err[3] = 64u;
+                    }
+                    ok = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(8);
+            }
+        }
+        sm.perm[6] = ok;
+    }
+    __syncthreads();
+    if (!sm.perm[6]) return;
+
     // ---- init (all waves), then one barrier; afterwards waves run freely
     for (int i = threadIdx.x; i < 3 * kRL * kWave; i += kThreads) (&sm.ewe[0][0][0])[i] = lds_empty_g();
     for (int i = threadIdx.x; i < kRL * kWave; i += kThreads) (&sm.inw[0][0])[i] = lds_empty_g();
-    for (int i = threadIdx.x; i < 4 * kRL * W; i += kThreads) (&sm.ins[0][0][0])[i] = lds_empty_g();
-    if (threadIdx.x < 8) sm.perm[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < 4 * kNI; i += kThreads) (&sm.ins[0][0])[i] = lds_empty_g();
+    if (threadIdx.x < 6) sm.perm[threadIdx.x] = 0;
+    if (threadIdx.x < 4) sm.prog[threadIdx.x] = 0;
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
@@ -236,15 +303,17 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             const d2 v = a.colc[(size_t)(tj0 + wave) * W + c];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
-        // state 0 of the lane's column c sits at diagonal c + lane - W (slot (c + lane) mod W)
-        const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
-                                                 (size_t)a.L * kWave * 16);
-        for (int c = 0; c < W; ++c) {
-            long long e = (a.origin + c + lane - W) % a.L;
-            e = e < 0 ? e + a.L : e;
-            const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
-            sm.st[wave][(c + lane) & (W - 1)][lane] = x0;
-            if constexpr (SWEEP) sm.st0[wave][(c + lane) & (W - 1)][lane] = x0;
+        if constexpr (!WIDE) {
+            // state 0 of the lane's column c sits at diagonal c + lane - W (slot (c + lane) mod W)
+            const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
+                                                     (size_t)a.L * kWave * 16);
+            for (int c = 0; c < W; ++c) {
+                long long e = (a.origin + c + lane - W) % a.L;
+                e = e < 0 ? e + a.L : e;
+                const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
+                sm.st[wave][(c + lane) & (W - 1)][lane] = x0;
+                if constexpr (SWEEP) sm.st0[wave][(c + lane) & (W - 1)][lane] = x0;
+            }
         }
     }
     __syncthreads();
@@ -252,10 +321,9 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     if (wave == 4) {
         // ================= comm wave =================
         __builtin_amdgcn_s_setprio(0);
-        constexpr int nS = 4 * W;      // south/north streams: (wave, column)
-        constexpr int P = kWave / nS;  // lanes (step phases) per stream
-        const int sidx = lane % nS, ph = lane / nS;
-        const int kS = sidx / W, cS = sidx - kS * W;
+        // south / north streams: lane = kS * 16 + jS handles the diagonals
+        // jS (mod 16) of wave kS's tile
+        const int kS = lane >> 4, jS = lane & (kSL - 1);
         const bool kval = kS < nval;
         const int tS = ti * ntj + tj0 + kS;  // this lane's tile (S/N groups)
         const bool actS = kval && (south_dev || south_host);
@@ -267,29 +335,46 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         const __amdgpu_buffer_rsrc_t sbox = rsrc(a.sbox, a.sbox_bytes);
         const __amdgpu_buffer_rsrc_t hin = rsrc(a.halo_in, a.halo_in ? a.halo_bytes : 0);
         const __amdgpu_buffer_rsrc_t hout = rsrc(a.halo_out, a.halo_out ? a.halo_bytes : 0);
-        // slot byte offsets (slot index added per step)
         // halo rings hold real columns only: a padding column (C >= nx) of a
         // boundary strip is served a zero inflow / granted at once
-        const int C = (tj0 + kS) * W + cS;
-        const bool virtS = south_host && C >= hcols, virtN = north_host && C >= hcols;
-        const unsigned sS = south_dev ? ((unsigned)tS * kR * W + cS) * G : (unsigned)C * 16u;
-        const unsigned sSstep = south_dev ? (unsigned)W * G : (unsigned)hcols * 16u;
-        const unsigned sN = north_dev ? ((unsigned)(tS + ntj) * kR * W + cS) * G : (unsigned)C * 16u;
-        const unsigned sNstep = north_dev ? (unsigned)W * G : (unsigned)hcols * 16u;
+        const int C0 = (tj0 + kS) * W;  // first global column of the lane's tile
+        const unsigned sSb = (unsigned)tS * kR * W * G;          // south box of the lane's tile
+        const unsigned sNb = (unsigned)(tS + ntj) * kR * W * G;  // south box of the north tile
         const unsigned sW = ((unsigned)(ti * ntj + tj0) * kR * kWave + lane) * G;
         const unsigned sE = ((unsigned)(ti * ntj + tj0 + 4) * kR * kWave + lane) * G;
         const unsigned sWEstep = (unsigned)kWave * G;
-        int qs = ph, qn = ph, qw = 0, qe = 0;
+        const int kq = kS & 3;
+        int qs = jS, qn = jS, qw = 0, qe = 0;  // qs, qn: diagonals; qw, qe: steps
         long long t_prog = now_rt();
         unsigned long long iters = 0;
         for (;;) {
-            const bool wS = actS && qs < K, wN = actN && qn < K;
-            const bool wW = actW && qw < K, wE = actE && qe < K;
-            if (!__any(wS || wN || wW || wE)) break;
+            const bool rS = actS && qs < KW, rN = actN && qn < KW;
+            const bool rW = actW && qw < K, rE = actE && qe < K;
+            if (!__any(rS || rN || rW || rE)) break;
             ++iters;
-            const int aS = a.qbase + qs, aN = a.qbase + qn, aW = a.qbase + qw, aE = a.qbase + qe;
-            const unsigned oS = wS && !virtS ? sS + (unsigned)(aS & (kR - 1)) * sSstep : kOOB;
-            const unsigned oN = wN && !virtN ? sN + (unsigned)(aN & (kR - 1)) * sNstep : kOOB;
+            // due: the consuming / producing compute wave is within kLA diagonals
+            const int pS = lds_ldi(&sm.prog[kq]);
+            const int p0 = lds_ldi(&sm.prog[0]);
+            const int p3 = lds_ldi(&sm.prog[3]);
+            const bool wS = rS && qs <= pS + kLA;
+            const bool wN = rN && qn + top <= pS + 2 * kLA;
+            const bool wW = rW && qw * W + lane <= p0 + kLA;
+            // (the east grant is a minimum over all rows: every row's slot of
+            // step qe is polled once row 0 approaches it)
+            const bool wE = rE && qe * W + (W - 1) <= p3 + 2 * kLA;
+            const int aS = a.qbase + (qs >> LW), aN = a.qbase + (qn >> LW);
+            const int aW = a.qbase + qw, aE = a.qbase + qe;
+            const int cS = qs & (W - 1), cN = qn & (W - 1);
+            const bool virtS = south_host && C0 + cS >= hcols;
+            const bool virtN = north_host && C0 + cN >= hcols;
+            const unsigned oS = wS && !virtS
+                                    ? (south_dev ? sSb + ((unsigned)(aS & (kR - 1)) * W + cS) * G
+                                                 : ((unsigned)(aS & (kR - 1)) * hcols + C0 + cS) * 16u)
+                                    : kOOB;
+            const unsigned oN = wN && !virtN
+                                    ? (north_dev ? sNb + ((unsigned)(aN & (kR - 1)) * W + cN) * G
+                                                 : ((unsigned)(aN & (kR - 1)) * hcols + C0 + cN) * 16u)
+                                    : kOOB;
             const unsigned oW = wW ? sW + (unsigned)(aW & (kR - 1)) * sWEstep : kOOB;
             const unsigned oE = wE ? sE + (unsigned)(aE & (kR - 1)) * sWEstep : kOOB;
             const v4u gS = south_host ? ld_sys(hin, oS) : ld_dev(sbox, oS);  // OOB: zeros
@@ -298,13 +383,13 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             const v4u gE = ld_dev(wbox, oE);
             bool prog = false;
             if (wS && g_is_data(gS)) {
-                v4u *slot = &sm.ins[kS][qs & (kRL - 1)][cS];
+                v4u *slot = &sm.ins[kq][qs & (kNI - 1)];
                 if (!l_is_data(lds_ld(slot))) {
                     lds_st(slot, gS);
                     const v4u e = sent_g(((aS / kR) & 1) ^ 1);
                     if (south_host) st_sys(hin, oS, e);  // (virtual: oS is OOB, dropped)
                     else st_dev(sbox, oS, e);
-                    qs += P;
+                    qs += kSL;
                     prog = true;
                 }
             }
@@ -318,40 +403,38 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
                 }
             }
             if (wN && (virtN || g_is_empty(gN, (aN / kR) & 1))) {
-                qn += P;
+                qn += kSL;
                 prog = true;
             }
             if (wE && g_is_empty(gE, (aE / kR) & 1)) {
                 ++qe;
                 prog = true;
             }
-            // grants: north of wave k = min over its streams (all phases)
+            // grants: north of wave k = the first diagonal not yet verified
+            // free over its 16 stream lanes; east of wave 3 = min over rows
             int vN = actN ? qn : INT_MAX;
-            for (int m = 1; m < W; m <<= 1) vN = min(vN, __shfl_xor(vN, m));
-            if (P == 2) vN = min(vN, __shfl_xor(vN, 32));
+            for (int m = 1; m < kSL; m <<= 1) vN = min(vN, __shfl_xor(vN, m));
             int vE = actE ? qe : INT_MAX;
             for (int m = 1; m < kWave; m <<= 1) vE = min(vE, __shfl_xor(vE, m));
-            if (ph == 0 && cS == 0 && kval) lds_sti(&sm.perm[kS], vN);
+            if (jS == 0 && kval) lds_sti(&sm.perm[kq], vN);
             if (lane == 0) lds_sti(&sm.perm[4], vE);
             const long long tn = now_rt();
-            if (__any(prog)) {
-                t_prog = tn;
-            } else {
-                if (tn - t_prog > a.spin_ticks) {
-                    if (lane == 0) {
-                        lds_sti(&sm.perm[5], 1);
-                        if (atomicOr(a.err, 1u) == 0) {
-                            a.err[1] = (unsigned)(ti * ntj + tj0);
-                            a.err[2] = (unsigned)min(min(wS ? qs : INT_MAX, wN ? qn : INT_MAX),
-                                                     min(wW ? qw : INT_MAX, wE ? qe : INT_MAX));
-                            a.err[3] = 16u | (__any(wS) ? 1u : 0u) | (__any(wW) ? 2u : 0u) |
-                                       (__any(wN) ? 4u : 0u) | (__any(wE) ? 8u : 0u);
-                        }
+            if (__any(prog) || !__any(wS || wN || wW || wE)) {
+                t_prog = tn;  // progress, or nothing due (the compute waves time out themselves)
+            } else if (tn - t_prog > a.spin_ticks) {
+                if (lane == 0) {
+                    lds_sti(&sm.perm[5], 1);
+                    if (atomicOr(a.err, 1u) == 0) {
+                        a.err[1] = (unsigned)(ti * ntj + tj0);
+                        a.err[2] = (unsigned)min(min(wS ? qs : INT_MAX, wN ? qn : INT_MAX),
+                                                 min(wW ? qw : INT_MAX, wE ? qe : INT_MAX));
+                        a.err[3] = 16u | (__any(wS) ? 1u : 0u) | (__any(wW) ? 2u : 0u) |
+                                   (__any(wN) ? 4u : 0u) | (__any(wE) ? 8u : 0u);
                     }
-                    break;
                 }
-                __builtin_amdgcn_s_sleep(2);
+                break;
             }
+            if (!__any(prog)) __builtin_amdgcn_s_sleep(2);
             if (lds_ldi(&sm.perm[5])) break;
         }
         if (lane == 0) atomicAdd(&a.stats->why[5], iters);
@@ -405,8 +488,22 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     const v4u lempty = lds_empty_g();
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
-    unsigned long long spins = 0, slow_n = 0, ieee_n = 0;
+    unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0;
     bool aborted = false;
+
+    // wide tiles: the previous state of diagonal s (ring entry s - W), kPf
+    // diagonals ahead; pr = ring entry of the next prefetch
+    v4u pf[WIDE ? kPf : 1];
+    long long pr = 0;
+    if constexpr (WIDE) {
+        pr = (a.origin - W) % L;
+        pr = pr < 0 ? pr + L : pr;
+#pragma unroll
+        for (int i = 0; i < kPf; ++i) {
+            pf[i] = ld_plain(ring, (unsigned)pr * 1024u + lane16);
+            pr = pr + 1 == L ? 0 : pr + 1;
+        }
+    }
 
     // LDS inputs of diagonal s, read at the end of diagonal s - 1
     struct In {
@@ -427,26 +524,25 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             in.nt = q >= qn;
             in.xs = (in.nt ? my_st0 : my_st)[(s & (W - 1)) * kWave + lane];
             in.src = (in.nt ? src_nxt : src_cur)[c];
-        } else {
+        } else if constexpr (!WIDE) {
             in.nt = false;
             in.xs = my_st[(s & (W - 1)) * kWave + lane];
+            in.src = 0.0;
+        } else {
+            in.nt = false;
             in.src = 0.0;
         }
         in.cs = sm.cc[k][c];
         in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
-        in.gs = lds_ld(has_south && s < KW ? &sm.ins[k][(s >> LW) & (kRL - 1)][s & (W - 1)] : &sm.zero);
+        in.gs = lds_ld(has_south && s < KW ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
         in.pn = lds_ldi(&sm.perm[k]);
         in.pe = lds_ldi(&sm.perm[4]);
         in.ee = east_lds ? lds_ld32((const char *)&sm.ewe[k][q & (kRL - 1)][lane] + 4) : kLdsEmptyHi;
         return in;
     };
-    const int total = KW + kWave - 1;
-    In in = fetch(0);
-    // Land the prologue's global loads (row coefficients) here: a first use
-    // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
-    // in flight -- into every diagonal.
-    __builtin_amdgcn_s_waitcnt(0);
-    for (int s = 0; s < total; ++s) {
+
+    // one diagonal; returns false when the launch is aborted
+    auto diagonal = [&](const int s, const int u, In &in) -> bool {
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -457,7 +553,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         const bool out_e = atE && valid && rowok;
         const bool out_n = lane == top && valid && has_north;
         // ---- inflow-independent part of the cell (MarchCell::pre, same op order)
-        const d2 x = as_d2(in.xs);
+        const d2 x = as_d2(WIDE ? pf[u % (WIDE ? kPf : 1)] : in.xs);
         const d2 co = as_d2(in.cs);
         const double pu = x.x, pv = x.y;
         const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
@@ -479,7 +575,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             bool b = (need_w && !l_is_data(v.gw)) || (lane == 0 && need_s && !l_is_data(v.gs));
             b |= east_lds && out_e && v.ee != kLdsEmptyHi;
             b |= east_glob && out_e && q >= v.pe;
-            b |= out_n && q >= v.pn;
+            b |= out_n && t >= v.pn;
             return b;
         };
         if (__builtin_expect(__any(blocked(in)), 0)) {
@@ -499,11 +595,9 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
                             a.err[3] = 32u;
                         }
                     }
-                    aborted = true;
-                    break;
+                    return false;
                 }
             }
-            if (aborted) break;
         }
         // ---- the cell's chain
         if (at0) {
@@ -520,6 +614,10 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         if (__builtin_expect(__any(!ok && valid && rowok), 0)) {
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             ++ieee_n;
+            // the only place a non-finite state can appear (the fast path's
+            // operands and results are finite by its range check)
+            if (__any(valid && rowok && !(__builtin_isfinite(o0) && __builtin_isfinite(o1))))
+                ++nonfin_n;
         }
         e0 = oe0;
         e1 = oe1;
@@ -527,24 +625,29 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         no1 = on1;
         // ---- outputs (lanes that have not started keep their step-0 state)
         const v4u out = as_v4u(o0, o1);
-        if (t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
+        if constexpr (!WIDE) {
+            if (t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
+        }
         st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
         pw = pw + 1 == L ? 0 : pw + 1;
         const v4u eo = as_v4u(oe0, oe1);
         const int aq = a.qbase + q;
         if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
-        if (east_glob) st_dev(wbox, out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
-        if (has_north) {
+        // wide tiles issue every store on every diagonal (out-of-range offsets
+        // are dropped), so the compiler's vmcnt for the prefetch is exact
+        if (WIDE || east_glob)
+            st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
+        if (WIDE || has_north) {
             const v4u no = as_v4u(on0, on1);
             const unsigned off = out_n && c < ncol_real
                                      ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
-                                       : kOOB;
+                                     : kOOB;
             if (north_host) st_sys(hout, off, no);
             else st_dev(sbox, off, no);
         }
         // consumed inbound slots back to empty
         if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
-        if (need_s && lane == 0) lds_st(&sm.ins[k][(s >> LW) & (kRL - 1)][s & (W - 1)], lempty);
+        if (need_s && lane == 0) lds_st(&sm.ins[k][s & (kNI - 1)], lempty);
         if constexpr (SWEEP) {
             // the lane finished the first step of its next trajectory: switch
             if (in.nt && atE) {
@@ -557,12 +660,32 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
+        if constexpr (WIDE) {
+            pf[u % (WIDE ? kPf : 1)] = ld_plain(ring, (unsigned)pr * 1024u + lane16);
+            pr = pr + 1 == L ? 0 : pr + 1;
+        }
         in = fetch(s + 1);
+        return true;
+    };
+
+    const int total = KW + kWave - 1;
+    In in = fetch(0);
+    // Land the prologue's global loads (row coefficients) here: a first use
+    // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
+    // in flight -- into every diagonal.
+    __builtin_amdgcn_s_waitcnt(0);
+    for (int sb = 0; sb < total && !aborted; sb += U) {
+        if (lane == 0) lds_sti(&sm.prog[k], sb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!aborted && !diagonal(sb + u, u, in)) aborted = true;
+        }
     }
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, spins);
         if (slow_n) atomicAdd(&a.stats->slow_diagonals, slow_n);
         if (ieee_n) atomicAdd(&a.stats->ieee_diagonals, ieee_n);
+        if (nonfin_n) atomicAdd(&a.stats->nonfinite_diagonals, nonfin_n);
         atomicAdd(&a.stats->tile_steps, (unsigned long long)K);
     }
 }
@@ -573,9 +696,60 @@ __global__ void pipe_fill_kernel(v4u *p, size_t n, int color)
     if (i < n) p[i] = sent_g(color);
 }
 
+template <bool SWEEP>
+const void *kernel_of(int W)
+{
+    switch (W) {
+    case 8: return (const void *)pipe_kernel<8, SWEEP>;
+    case 16: return (const void *)pipe_kernel<16, SWEEP>;
+    default: break;
+    }
+    if constexpr (!SWEEP) {
+        switch (W) {
+        case 32: return (const void *)pipe_kernel<32, false>;
+        case 64: return (const void *)pipe_kernel<64, false>;
+        case 128: return (const void *)pipe_kernel<128, false>;
+        case 256: return (const void *)pipe_kernel<256, false>;
+        case 512: return (const void *)pipe_kernel<512, false>;
+        case 1024: return (const void *)pipe_kernel<1024, false>;
+        default: break;
+        }
+    }
+    return nullptr;
+}
+
+const void *pipe_fn(int W, bool sweep) { return sweep ? kernel_of<true>(W) : kernel_of<false>(W); }
+
+// dynamic LDS that pins the wide-tile engine to `per_cu` workgroups per CU
+// (its static image is small enough for several); narrow tiles keep theirs
+size_t pipe_dyn_lds(int W, const void *fn, int per_cu)
+{
+    if (W <= 16) return 0;
+    hipFuncAttributes at{};
+    if (hipFuncGetAttributes(&at, fn) != hipSuccess) return 0;
+    const size_t lds_cu = 160 * 1024;
+    const size_t want = lds_cu / (size_t)(per_cu + 1) + 1024;
+    if (want > lds_cu / (size_t)per_cu) return 0;
+    return at.sharedSizeBytes >= want ? 0 : want - at.sharedSizeBytes;
+}
+
+int pipe_per_cu_opt()
+{
+    static int v = -1;
+    if (v < 0) {
+        v = 1;
+        if (const char *e = std::getenv("BURG_PIPE_WG_PER_CU")) {  // tuning knob
+            const int x = std::atoi(e);
+            if (x >= 1 && x <= 2) v = x;
+        }
+    }
+    return v;
+}
+
 }  // namespace
 
-bool pipe_width_supported(int W) { return W == 8 || W == 16; }
+bool pipe_width_supported(int W) { return pipe_fn(W, false) != nullptr; }
+bool pipe_sweep_width_supported(int W) { return pipe_fn(W, true) != nullptr; }
 
 // resident workgroups of the pipe kernel (sweep = the burg_sweep variant,
 // whose larger LDS image must also fit one workgroup per CU)
@@ -585,9 +759,10 @@ int pipe_max_resident_blocks(int W, bool sweep)
     if (hipGetDevice(&dev) != hipSuccess) return -3;
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return -3;
-    const void *fn = W == 8 ? (sweep ? (const void *)pipe_kernel<8, true> : (const void *)pipe_kernel<8, false>)
-                            : (sweep ? (const void *)pipe_kernel<16, true> : (const void *)pipe_kernel<16, false>);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, 0) != hipSuccess) return -3;
+    const void *fn = pipe_fn(W, sweep);
+    if (!fn) return -1;
+    const size_t dyn = pipe_dyn_lds(W, fn, pipe_per_cu_opt());
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, dyn) != hipSuccess) return -3;
     return n * ncu;
 }
 
@@ -596,16 +771,14 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     const int blocks = a.nti * a.nwj;
     const bool sweep = a.colc_b != nullptr;
     if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
-    if (W == 8 && !sweep)
-        hipLaunchKernelGGL((pipe_kernel<8, false>), dim3(blocks), dim3(kThreads), 0, st, a);
-    else if (W == 8)
-        hipLaunchKernelGGL((pipe_kernel<8, true>), dim3(blocks), dim3(kThreads), 0, st, a);
-    else if (W == 16 && !sweep)
-        hipLaunchKernelGGL((pipe_kernel<16, false>), dim3(blocks), dim3(kThreads), 0, st, a);
-    else if (W == 16)
-        hipLaunchKernelGGL((pipe_kernel<16, true>), dim3(blocks), dim3(kThreads), 0, st, a);
-    else
-        return -1;
+    const void *fn = pipe_fn(W, sweep);
+    if (!fn) return -1;
+    const size_t dyn = pipe_dyn_lds(W, fn, pipe_per_cu_opt());
+    // the census counter starts at zero in every launch
+    if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;
+    PipeArgs args = a;
+    void *kargs[] = {&args};
+    if (hipLaunchKernel(fn, dim3(blocks), dim3(kThreads), kargs, dyn, st) != hipSuccess) return -3;
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

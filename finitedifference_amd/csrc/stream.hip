@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
     __builtin_amdgcn_s_waitcnt(0);
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
-    unsigned spins = 0, slow_n = 0, why_n[6] = {0, 0, 0, 0, 0, 0};
+    unsigned spins = 0, slow_n = 0, nonfin_n = 0, why_n[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long slow_t = 0;
     bool bad_range = false;
 
@@ -337,6 +337,9 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
             n1 = shr1_or(as_d2(gs[m]).y, no1);
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             bad_range = true;
+            // the only place a non-finite state can appear (fast-path range check)
+            if (__any(valid && rowok && !(__builtin_isfinite(o0) && __builtin_isfinite(o1))))
+                ++nonfin_n;
             ++slow_n;
             slow_t += __builtin_amdgcn_s_memtime() - t_in;
         }
@@ -373,6 +376,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
                 if (why_n[q]) atomicAdd(&a.stats->why[q], (unsigned long long)why_n[q]);
         }
         atomicAdd(&a.stats->tile_steps, (unsigned long long)a.K);
+        if (nonfin_n) atomicAdd(&a.stats->nonfinite_diagonals, (unsigned long long)nonfin_n);
     }
     if (__any(bad_range) && lane == 0) atomicAdd(&a.stats->ieee_diagonals, 1ull);
 }

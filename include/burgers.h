@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 6
+#define BURG_ABI_VERSION 7
 
 enum burg_status {
     BURG_OK = 0,
@@ -94,6 +94,8 @@ typedef struct burg_stats {
     int64_t slow_ticks;         /* streaming engine: shader clocks spent on the slow path */
     int64_t ieee_diagonals;     /* stream/pipe: diagonals redone with IEEE sqrt/div (range) */
     int64_t comm_polls;         /* pipe engine: comm-wave polling rounds (all workgroups) */
+    int64_t nonfinite_diagonals; /* stream/pipe: diagonals whose new state held a NaN/Inf
+                                    (the call then returns BURG_ENAN) */
 } burg_stats;
 
 enum burg_engine {

@@ -1,6 +1,12 @@
-"""One rank of tests/test_gpu_parity.py::test_slab_halo_two_processes_one_gpu
-(not a test module): its slab of an N x N grid, T steps from w0 = 1, on
-device 0, rendezvous over gloo; writes its slab snapshot matrix."""
+"""One rank of the slab tests in tests/test_gpu_parity.py (not a test module):
+its slab of an NX x NY grid (default N x N), T steps from w0 = 1, on device 0,
+rendezvous over gloo; writes its slab snapshot matrix.
+
+    slab_worker.py N T OUTDIR [run|sweep]
+    env: SLAB_NY (rows, default N), SLAB_W (pipe tile width, 0 = plan),
+         SLAB_TILES (tiles target per rank), SLAB_SNAP_EVERY (default 1),
+         SLAB_DT (default 0.05)
+"""
 import os
 import sys
 
@@ -15,24 +21,33 @@ SWEEP_MUS = [(4.25, 0.015), (5.19, 0.026), (5.5, 0.03)]
 def main():
     N, T, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     sweep = len(sys.argv) > 4 and sys.argv[4] == "sweep"  # mu sweep (burg_sweep) instead
+    ny = int(os.environ.get("SLAB_NY", N))
+    W = int(os.environ.get("SLAB_W", "0"))
+    tiles = int(os.environ.get("SLAB_TILES", "0"))
+    every = int(os.environ.get("SLAB_SNAP_EVERY", "1"))
+    dt = float(os.environ.get("SLAB_DT", "0.05"))
     import torch.distributed as dist
     from finitedifference_amd.dist import make_slab_context, slab_state
     dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
-    ctx = make_slab_context(N, N, rank, world, device=0, dist=dist)
-    g = np.linspace(0, 100, N + 1)
-    ctx.set_problem(g, g, 0.05, (5.19, 0.026))
-    w0 = slab_state(np.ones(2 * N * N), N, N, rank, world)
+    ctx = make_slab_context(N, ny, rank, world, device=0, dist=dist, stream_w=W,
+                            tiles_target=tiles)
+    gx = np.linspace(0, 100, N + 1)
+    gy = np.linspace(0, 100.0 * ny / N, ny + 1)
+    ctx.set_problem(gx, gy, dt, (5.19, 0.026), allow_nonsquare=(ny != N))
+    w0 = slab_state(np.ones(2 * N * ny), N, ny, rank, world)
     dist.barrier()
     if sweep:
-        snaps, st = ctx.sweep(SWEEP_MUS, T, w0=w0)
+        snaps, st = ctx.sweep(SWEEP_MUS, T, w0=w0, snap_every=every)
         assert st["engine"] == 2
         for j, sn in enumerate(snaps):
             np.save(os.path.join(out, f"slab{rank}_mu{j}.npy"), sn)
     else:
-        snaps, st, _, _ = ctx.run(w0, T)
+        snaps, st, _, _ = ctx.run(w0, T, snap_every=every)
         assert st["engine"] == 2
         np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
+    with open(os.path.join(out, f"slab{rank}.w"), "w") as f:
+        f.write(str(st["stream_w"]))
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()

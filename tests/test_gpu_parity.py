@@ -396,6 +396,187 @@ def test_slab_halo_sweep_two_processes_one_gpu(gpu, orc, tmp_path):
             assert np.array_equal(snaps[:, k], ref[k]), f"mu {mu} step {k}"
 
 
+def _run_slabs(tmp_path, N, T, world, mode="run", timeout=110, **env_extra):
+    """Start `world` slab_worker processes on device 0 (gloo rendezvous) and
+    wait for them; env_extra: SLAB_NY, SLAB_W, SLAB_TILES, SLAB_SNAP_EVERY."""
+    import subprocess
+    import sys
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    worker = os.path.join(os.path.dirname(__file__), "slab_worker.py")
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20",
+                   **{k: str(v) for k, v in env_extra.items()})
+        procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path),
+                                       mode], env=env))
+    codes = []
+    for p in procs:
+        try:
+            codes.append(p.wait(timeout=timeout))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert codes == [0] * world, codes
+
+
+# ------------------------------------------------- pipe engine, wide tiles --
+@pytest.mark.parametrize("N,ny,W,T", [
+    (300, 300, 32, 4), (520, 300, 64, 3), (1000, 130, 128, 3), (700, 200, 256, 2),
+    (2100, 64, 512, 2), (1500, 100, 1024, 2), (333, 129, 256, 3)])
+def test_pipe_wide_bitwise_sequential_march(gpu, orc, N, ny, W, T):
+    """Wide tiles (previous state streamed from the HBM ring, not LDS): every
+    snapshot bit-equal to the oracle's sequential march -- partial tiles
+    (nx not a multiple of W), partial strips, one tile column, non-square."""
+    P = orc.Problem(N, ny, Ly=100.0 * ny / N, allow_nonsquare=(N != ny))
+    w0 = state_after(orc, P, 3)
+    ctx = FOMContext_for(N, ny, engine="pipe", stream_w=W)
+    ctx.set_problem(P.grid_x, P.grid_y, P.dt, P.mu, allow_nonsquare=(N != ny))
+    snaps, st, its, _ = ctx.run(w0, T)
+    ref, _, _ = P.fom(w0, T)
+    assert st["engine"] == 2 and st["stream_w"] == W
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+    assert st["tile_marches"] == T * st["stream_tiles"]
+    assert st["nonfinite_diagonals"] == 0
+
+
+def test_pipe_4096_bitwise(gpu, orc):
+    """BASELINE config 3 (4096^2, one GPU) on the engine the planner picks
+    (pipe, W = 256: 1024 tiles): 3 steps from w0 = 1, bit-equal to the oracle."""
+    N, T = 4096, 3
+    P = orc.Problem(N)
+    ctx = make_ctx(N)
+    snaps, st, _, _ = ctx.run(np.ones(P.m), T)
+    assert st["engine"] == 2 and st["stream_w"] == 256 and st["stream_tiles"] == 1024
+    ref, _, _ = P.fom(np.ones(P.m), T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+
+
+def test_pipe_4096_trajectory_matches_run(gpu, orc):
+    """The bench's unit of work at 4096^2 (burg_trajectory, state resident in
+    HBM) leaves the same final state as burg_run."""
+    N, T = 4096, 4
+    ctx = make_ctx(N)
+    w0 = np.ones(2 * N * N)
+    snaps, _, _, _ = ctx.run(w0, T, snap_every=T)
+    ctx.upload(w0)
+    st = ctx.trajectory(T)
+    assert st["engine"] == 2 and st["stream_w"] == 256
+    assert np.array_equal(ctx.download(), snaps[:, 1])
+
+
+def test_pipe_8192_chunked_property(gpu, monkeypatch):
+    """8192^2 on one GPU (W = 1024, 1024 tiles): a run forced into 2-step
+    launches; size-independent property: the last step solves the reference
+    residual, R(w_n+1; w_n) / R(w_n; w_n) < 1e-13.  dt = 0.05 * 1024 / N keeps
+    the 1024^2 configuration's CFL number: with dt = 0.05 the reference
+    scheme itself turns v negative at the boundary (dt > 2h) and reaches NaN
+    within a few steps at N >= 4096 (oracle)."""
+    N, T = 8192, 3
+    monkeypatch.setenv("BURG_STREAM_CHUNK", "2")
+    ctx = make_ctx(N, dt=0.05 * 1024 / N)
+    snaps, st, _, _ = ctx.run(np.ones(2 * N * N), T)
+    assert st["engine"] == 2 and st["stream_launches"] == 2 and st["stream_w"] == 1024
+    _, n0 = ctx.residual(snaps[:, T - 1], snaps[:, T - 1])
+    _, n1 = ctx.residual(snaps[:, T], snaps[:, T - 1])
+    assert n1 / n0 < 1e-13, (n1, n0)
+
+
+def test_sweep_1024_bench_config_bitwise(gpu, orc):
+    """The headline configuration's kernel (pipe_kernel<16, true>, 1024^2,
+    the 9 training mu of get_snapshot_params, 256 workgroups): 3 steps per
+    trajectory, each trajectory bit-equal to the oracle's march for its mu."""
+    from finitedifference_amd.config import get_snapshot_params
+    N, T = 1024, 3
+    mus = get_snapshot_params()[:9]
+    ctx = make_ctx(N)
+    snaps, st = ctx.sweep(mus, T, w0=np.ones(2 * N * N))
+    assert st["engine"] == 2 and st["stream_w"] == 16 and st["stream_launches"] == 1
+    for mu, sn in zip(mus, snaps):
+        ref, _, _ = orc.Problem(N, mu=tuple(mu)).fom(np.ones(2 * N * N), T)
+        for j in range(T + 1):
+            assert np.array_equal(sn[:, j], ref[j]), f"mu={mu} step {j}"
+
+
+def test_sweep_wide_tiles_one_launch_per_mu(gpu, orc):
+    """burg_sweep on wide tiles (no sweep kernel): one launch per mu, each
+    trajectory bit-equal to the oracle."""
+    N, ny, T = 600, 130, 3
+    mus = [(4.25, 0.015), (5.19, 0.026), (5.5, 0.03)]
+    P0 = orc.Problem(N, ny, Ly=100.0 * ny / N, allow_nonsquare=True)
+    ctx = FOMContext_for(N, ny, engine="pipe", stream_w=128)
+    ctx.set_problem(P0.grid_x, P0.grid_y, P0.dt, P0.mu, allow_nonsquare=True)
+    snaps, st = ctx.sweep(mus, T, w0=np.ones(P0.m))
+    assert st["stream_w"] == 128 and st["stream_launches"] == 3
+    for mu, sn in zip(mus, snaps):
+        P = orc.Problem(N, ny, mu=mu, Ly=100.0 * ny / N, allow_nonsquare=True)
+        ref, _, _ = P.fom(np.ones(P.m), T)
+        for j in range(T + 1):
+            assert np.array_equal(sn[:, j], ref[j]), f"mu={mu} step {j}"
+
+
+@pytest.mark.parametrize("engine", ["pipe", "stream"])
+def test_nan_in_w0_raises_enan(gpu, engine):
+    """A NaN planted in w0 makes the march report BURG_ENAN (SURVEY.md 5,
+    failure detection) instead of silently writing NaN snapshots."""
+    from finitedifference_amd._lib import BurgersError, BURG_ENAN
+    N = 96
+    ctx = make_ctx(N, engine=engine)
+    w0 = np.ones(2 * N * N)
+    w0[N * 40 + 17] = np.nan
+    with pytest.raises(BurgersError) as ei:
+        ctx.run(w0, 2)
+    assert ei.value.code == BURG_ENAN
+    snaps, st, _, _ = ctx.run(np.ones(2 * N * N), 2)  # the context stays usable
+    assert st["nonfinite_diagonals"] == 0 and np.isfinite(snaps).all()
+
+
+def test_slab_wide_rows_two_processes_one_gpu(gpu, orc, tmp_path):
+    """Multi-GPU slabs with 8192-wide rows (the per-GPU row length of BASELINE
+    config 4), rehearsed as 2 processes on one GPU (each limited to 512 tiles,
+    so both grids are resident together -> wide tiles): the assembled
+    trajectory is the single-domain march bit for bit."""
+    N, ny, T, world = 8192, 256, 3, 2
+    dt = 0.05 * 1024 / N  # the 1024^2 CFL (see test_pipe_8192_chunked_property)
+    _run_slabs(tmp_path, N, T, world, SLAB_NY=ny, SLAB_TILES=512, SLAB_DT=repr(dt))
+    widths = {open(os.path.join(tmp_path, f"slab{r}.w")).read() for r in range(world)}
+    assert widths == {"32"}, widths
+    from finitedifference_amd.dist import assemble_snaps
+    parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
+    snaps = assemble_snaps(parts, N, ny)
+    P = orc.Problem(N, ny, dt=dt, Ly=100.0 * ny / N, allow_nonsquare=True)
+    ref, _, _ = P.fom(np.ones(P.m), T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+
+
+def test_fine750_eight_uneven_slabs_one_gpu(gpu, orc, tmp_path):
+    """SURVEY.md 8(d) C5 parity case on one GPU: 750^2 over 8 slab processes
+    (uneven 94/93-row slabs), 500 steps with snap_every=100: assembled
+    snapshots bit-equal to the single-domain march and within 1e-10 of the
+    author's Fine HDM slices (F/run_fom.py:28, F/predict_mu_5.19e+00_2.60e-02_hprom.pickle)."""
+    N, T, world = 750, 500, 8
+    _run_slabs(tmp_path, N, T, world, timeout=300, SLAB_SNAP_EVERY=100)
+    from finitedifference_amd.dist import assemble_snaps, slab_rows
+    assert [slab_rows(N, world, r)[1] for r in range(world)] == [94] * 6 + [93] * 2
+    parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
+    snaps = assemble_snaps(parts, N, N)
+    g = golden("author_pickles.npz")
+    n = N * N
+    U = snaps[:n].reshape(N, N, -1)
+    for k in range(6):
+        assert rel(U[N // 2, :, k], g["fine_u_row"][k]) <= REF_TOL
+        assert rel(U[:, N // 2, k], g["fine_u_col"][k]) <= REF_TOL
+    single = make_ctx(N).run(np.ones(2 * n), T, snap_every=100)[0]
+    assert np.array_equal(snaps, single)
+
+
 def test_trajectory_from_initial_is_repeatable(gpu, orc):
     """burg_trajectory (the bench's unit of work): from the uploaded w0 every
     time, or continuing from the resident state; final states = oracle."""
