@@ -4,31 +4,34 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--time-steps T]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Unit of work ("step"): ONE SNAPSHOT SWEEP = the reference's FOM snapshot
-generation for the ROM training set (C/run_prom.py:59-71 ->
-load_or_compute_snaps for each of the 9 get_snapshot_params mu,
-C/train_autoencoder.py:63-72; each one run_fom.main's time loop,
-inviscid_burgers_implicit2D, C/hypernet2D.py:72-131): 9 trajectories of
-T = 500 implicit time steps (dt = 0.05, w0 = 1) of the whole grid, every
-intermediate state kept resident in HBM (the 9 snapshot matrices, engine ring
-layout), solved exactly by the HIP march in ONE pipelined launch
-(burg_sweep).  --sweep 1 times single trajectories at mu = (5.19, 0.026)
-(burg_trajectory) instead.
+Unit of work ("step"): ONE FOM TRAJECTORY = run_fom.main's time loop
+(inviscid_burgers_implicit2D, C/hypernet2D.py:72-131): T = 500 implicit time
+steps of the whole grid from w0 = 1 at mu = (5.19, 0.026), every intermediate
+state kept resident in HBM (the snapshot matrix, engine ring layout), solved
+exactly by the HIP march in ONE pipelined launch (burg_trajectory).
+--sweep N times the snapshot sweep over the first N training mu instead
+(burg_sweep; C/run_prom.py:59-71).
 
-Workload (BASELINE.json configs[1]): 1024 x 1024 cells per GPU, fp64.  N > 1:
-weak scaling by row slabs, rank k owning rows [1024k, 1024k+1024) of a
-1024 x 1024N grid (same cell size), the one-way halo streamed GPU-to-GPU
-during the launch.  value = N * 1024^2 * T * 9 * K / (max
-over ranks of the wall time of the K timed sweeps), inputs resident in HBM.
+Workload (BASELINE.json configs[2], the largest single-GPU config): 4096 x
+4096 cells per GPU, fp64.  dt = 0.05 * 1024 / nx: the CFL number of the
+1024^2 configuration (dt = 0.05 there, as run_fom.py).  With dt = 0.05 at
+4096^2 the reference scheme itself is unstable (dt > 2h: v < 0 at the
+boundary, NaN after 14 steps -- measured with the oracle),
+so a fixed dt would time NaN arithmetic.  N > 1: weak scaling by row slabs,
+rank k owning rows [4096k, 4096k + 4096) of a 4096 x 4096N grid (same cell
+size, same dt), the one-way halo streamed GPU-to-GPU during the launch
+(DESIGN.md section 7).  value = N * 4096^2 * T * K / (max over ranks of the
+wall time of the K timed trajectories), inputs resident in HBM.
 
 Extra JSON objects: roofline (the march kernel: algorithmic 32 B per
 cell-update = read the previous state u, v + write the new state u, v,
 SURVEY.md section 8(d); per-launch device time from HIP events on the
 library's stream; peak 8 TB/s; traffic from the committed rocprofv3 PMC
-passes, profiles/pmc_traffic.json) and cpu_baseline (the oracle's CPU
-restatement of the reference Newton algorithm, rank 0 at N = 1, bounded
-sample).  Only the cpu_baseline leg touches oracle/.  rom_pipeline: secondary
-numbers of the reference's ROM driver at 250^2 (sweep, POD, LSPG; --no-rom skips).
+passes, profiles/pmc_traffic.json), cpu_baseline (the oracle's CPU
+restatement, rank 0 at N = 1, bounded sample) and config2_1024 (BASELINE
+configs[1]: the 1024^2 9-mu snapshot sweep).  Only the cpu_baseline leg
+touches oracle/.  rom_pipeline: secondary numbers of the reference's ROM
+driver at 250^2 (sweep, POD, LSPG; --no-rom skips).
 """
 import argparse
 import json
@@ -53,12 +56,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10, help="timed sweeps")
     ap.add_argument("--warmup", type=int, default=2, help="untimed sweeps")
-    ap.add_argument("--sweep", type=int, default=9,
+    ap.add_argument("--sweep", type=int, default=1,
                     help="trajectories per step: the first N of the 9 training mu "
                          "(get_snapshot_params); 1 = one trajectory at mu=(5.19, 0.026)")
     ap.add_argument("--time-steps", type=int, default=500,
                     help="implicit steps per trajectory (run_fom.py: 500)")
-    ap.add_argument("--nx", type=int, default=1024)
+    ap.add_argument("--nx", type=int, default=4096)
+    ap.add_argument("--dt", type=float, default=None,
+                    help="time step (default 0.05 * 1024 / nx: the 1024^2 config's CFL)")
+    ap.add_argument("--no-1024", action="store_true",
+                    help="skip the secondary BASELINE configs[1] line (1024^2 9-mu sweep)")
     ap.add_argument("--rows-per-gpu", type=int, default=None)
     ap.add_argument("--engine", default="pipe", choices=["pipe", "stream"])
     ap.add_argument("--stream-w", type=int, default=0)
@@ -83,12 +90,12 @@ def dist_env():
     return rank, world, local
 
 
-def cpu_baseline(nx, seconds):
+def cpu_baseline(nx, dt, seconds):
     """Oracle restatement of the reference algorithm (newton_raphson + exact
     block solve, C/hypernet2D.py:72-131,1811-1857) on the host, 1 thread,
-    first steps of the same 1024^2 trajectory until `seconds` elapse."""
+    first steps of the same trajectory until `seconds` elapse."""
     from oracle import oracle
-    P = oracle.Problem(nx)
+    P = oracle.Problem(nx, dt=dt)
     w = np.ones(P.m)
     t0 = time.perf_counter()
     steps = 0
@@ -97,12 +104,12 @@ def cpu_baseline(nx, seconds):
         steps += 1
         if time.perf_counter() - t0 >= seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": nx * nx * steps / dt / 1e6, "unit": "Mcell-updates/s", "cores": 1,
-            "kind": "port",
+    el = time.perf_counter() - t0
+    return {"value": nx * nx * steps / el / 1e6, "unit": "Mcell-updates/s", "cores": 1,
+            "kind": "port", "nproc": os.cpu_count(),
             "sample": f"oracle Newton (reference algorithm, exact block solve in place of "
-                      f"SuperLU) on {nx}x{nx}, first {steps} of the 500 steps from w0=1, "
-                      f"{dt:.1f} s, 1 thread"}
+                      f"SuperLU) on {nx}x{nx}, dt={dt:g}, first {steps} of the 500 steps from "
+                      f"w0=1, {el:.1f} s, 1 thread"}
 
 
 def stencil_roofline(nx, reps=20, pmc_file=None):
@@ -194,6 +201,7 @@ def main():
     rows = args.rows_per_gpu or nx
     ny = rows * world
     T = args.time_steps
+    dt = args.dt if args.dt is not None else DT * 1024.0 / nx
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
     import torch
@@ -213,7 +221,7 @@ def main():
                             stream_w=args.stream_w)
     gx = np.linspace(0, 100, nx + 1)
     gy = np.linspace(0, 100.0 * ny / nx, ny + 1)  # same cell size: weak scaling
-    ctx.set_problem(gx, gy, DT, MU, allow_nonsquare=(nx != ny))
+    ctx.set_problem(gx, gy, dt, MU, allow_nonsquare=(nx != ny))
     ctx.upload(np.ones(ctx.m))
     from finitedifference_amd.config import get_snapshot_params
     mus = get_snapshot_params()[:args.sweep] if args.sweep > 1 else [MU]
@@ -250,7 +258,10 @@ def main():
     cells = nx * ny  # whole job
     value = cells * T * nmu * args.steps / elapsed / 1e6
 
+    st_main = st
+    ctx.close()  # give the trajectory ring back before the secondary probes
     if rank == 0:
+        st = st_main
         eng = {0: "stream", 2: "pipe"}.get(st["engine"], str(st["engine"]))
         kname = (f"pipe_kernel<{st['stream_w']}, {'true' if nmu > 1 else 'false'}>"
                  if st["engine"] == 2 else f"stream_kernel<{st['stream_w']}>")
@@ -260,6 +271,10 @@ def main():
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
         key = f"{eng}:{nx}x{rows}:T{T}" + (f"x{nmu}" if nmu > 1 else "")
         traffic, tsrc = read_pmc(args.pmc_file, key)
+        what = (f"the FOM snapshot sweep over the first {nmu} training mu of get_snapshot_params "
+                f"(C/train_autoencoder.py:63-72, as run_prom.py:59-71), {T} steps each"
+                if nmu > 1 else
+                f"one {T}-step FOM trajectory from w0 at mu=(5.19,0.026) (run_fom.main's loop)")
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -272,18 +287,14 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": ("synthetic: reference initial state w0=1, dt=0.05; each step = the FOM "
-                     f"snapshot sweep over the first {nmu} training mu of get_snapshot_params "
-                     f"(C/train_autoencoder.py:63-72, as run_prom.py:59-71), {T} steps each"
-                     if nmu > 1 else
-                     "synthetic: reference initial state w0=1, mu=(5.19,0.026), dt=0.05; "
-                     "each step = one 500-step FOM trajectory from w0 (run_fom.main's loop)"),
+            "data": (f"synthetic: reference initial state w0=1, dt={dt:g} (0.05*1024/nx: the "
+                     f"1024^2 config's CFL), domain cell size 100/{nx}; each step = {what}"),
             "config": {
                 "workload": f"implicit 2D inviscid Burgers FOM (run_fom time loop), "
                             f"{nx}x{rows} cells per GPU (grid {nx}x{ny}), fp64, "
                             f"{T} implicit steps per trajectory, {nmu} trajectories (mu) "
-                            f"per step, exact march on MI355X",
-                "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T,
+                            f"per step, exact march on MI355X (BASELINE configs[2] at N=1)",
+                "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T, "dt": dt,
                 "trajectories_per_step": nmu,
                 "parallelism": f"row-slab x{world}",
             },
@@ -302,17 +313,49 @@ def main():
                 "traffic_source": tsrc,
             },
         }
+        if world == 1 and not args.no_1024:
+            out["config2_1024"] = config2_1024(args.pmc_file)
         if world == 1 and args.stencil_nx > 0:
             out["stencil_roofline"] = stencil_roofline(args.stencil_nx, pmc_file=args.pmc_file)
         if world == 1 and not args.no_rom:
             out["rom_pipeline"] = rom_pipeline()
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(nx, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(nx, dt, args.cpu_seconds)
         print(json.dumps(out), flush=True)
-    ctx.close()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def config2_1024(pmc_file, steps=3):
+    """BASELINE configs[1] (1024^2, dt = 0.05 as run_fom.py): the 9-mu FOM
+    snapshot sweep in one burg_sweep launch (pipe_kernel<16, true>), every
+    state kept in HBM; secondary to the headline."""
+    from finitedifference_amd.config import get_snapshot_params
+    from finitedifference_amd.solver import FOMContext
+    nx, T = 1024, 500
+    mus = get_snapshot_params()[:9]
+    ctx = FOMContext(nx, nx, engine="pipe")
+    g = np.linspace(0, 100, nx + 1)
+    ctx.set_problem(g, g, DT, MU)
+    ctx.upload(np.ones(ctx.m))
+    ctx.sweep(mus, T, keep_snaps=False)
+    t0 = time.perf_counter()
+    kern = 0.0
+    for _ in range(steps):
+        st = ctx.sweep(mus, T, keep_snaps=False)[1]
+        kern += st["loop_ms"]
+    el = time.perf_counter() - t0
+    ctx.close()
+    upd = nx * nx * T * len(mus)
+    ms = kern / steps
+    gbs = BYTES_PER_CELL_UPDATE * upd / (ms * 1e-3) / 1e9
+    traffic, tsrc = read_pmc(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
+    return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
+            "value": round(upd * steps / el / 1e6, 3), "unit": "Mcell-updates/s",
+            "kernel": f"pipe_kernel<{st['stream_w']}, true>", "avg_launch_ms": round(ms, 4),
+            "roofline_frac": round(gbs / HBM_PEAK_GBS, 5), "achieved_GBs": round(gbs, 1),
+            "ieee_diagonals": st["ieee_diagonals"], "traffic": traffic, "traffic_source": tsrc}
 
 
 if __name__ == "__main__":

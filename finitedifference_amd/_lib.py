@@ -27,7 +27,7 @@ EXPORTS = (
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_lspg",
-    "burg_pod", "burg_pod_rsvd",
+    "burg_pod", "burg_pod_rsvd", "burg_run_npy",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -132,6 +132,8 @@ def load(path=None):
             "burg_pod_rsvd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int, _D,
                                              ctypes.c_int, ctypes.c_int, ctypes.c_int, _D, _D, _D,
                                              _D]),
+            "burg_run_npy": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                            ctypes.POINTER(BurgStats)]),
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),

@@ -135,6 +135,8 @@ struct PipeArgs {
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid
+    int dbg;              // diagnostics (BURG_PIPE_DEBUG): bit 0 = check the wide state window
+    double *dbgbuf;       // diagnostics: 32 doubles (bit 2: tile 0, lane 0, diagonal 0 inputs)
     unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)
     unsigned *census;     // workgroups checked in (zeroed before every launch)
     StreamStats *stats;
@@ -168,6 +170,8 @@ int launch_colc_batch(const Coeffs &cf, int nb, const double *src_b, int ncols_p
                       hipStream_t st);
 int launch_fill_sentinel(void *p, size_t n16, hipStream_t st);
 int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st);
+int launch_ring_extract_rows(const StreamArgs &a, int W, size_t e0, size_t ne, int k0, int kstep,
+                             int ncols, double *out, hipStream_t st);
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
                         int ldo, hipStream_t st);
 bool pipe_width_supported(int W);

@@ -11,7 +11,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <fcntl.h>
@@ -496,6 +499,12 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
     a.err = c->d_err;
     a.census = c->d_err + 4;
+    if (const char *e = std::getenv("BURG_PIPE_DEBUG")) {  // diagnostics
+        a.dbg = std::atoi(e);
+        static double *dbgbuf = nullptr;
+        if ((a.dbg & 4) && !dbgbuf) (void)hipMalloc((void **)&dbgbuf, 32 * sizeof(double));
+        a.dbgbuf = dbgbuf;
+    }
     a.stats = c->d_sstats;
     if (c->ov_colc) a.colc = c->ov_colc;
     if (c->ov_lbc) a.cf.lbc = c->ov_lbc;
@@ -516,6 +525,18 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
     float t = 0.f;
     HIPCHK(hipEventElapsedTime(&t, c->ev0, c->ev1));
     *ms += t;
+    if (pipe) {
+        const PipeArgs pa = pipe_args(c, L, origin, K);
+        if ((pa.dbg & 4) && pa.dbgbuf) {
+            double v[24];
+            (void)hipMemcpy(v, pa.dbgbuf, sizeof v, hipMemcpyDeviceToHost);
+            std::fprintf(stderr, "[pipe dbg] loader: win[0][0][0] %g %g ring %g %g e %g L %g "
+                         "origin %g nf %g\n", v[16], v[17], v[18], v[19], v[20], v[21], v[22], v[23]);
+            std::fprintf(stderr, "[pipe dbg] pu %g pv %g hx %g src %g sl %g ay %g lb %g e %g %g n %g %g "
+                         "o %g %g bu %g bv %g ok %g\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7],
+                         v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15]);
+        }
+    }
     unsigned err[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
     if (err[0]) {
@@ -538,7 +559,8 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
             return fail(BURG_EHIP,
                         "pipe engine: a wait timed out (workgroup tile %u of %d, step/diagonal %u, "
                         "wait %#x [16: comm wave: 1 south 2 west 4 north-grant 8 east-grant; 32: "
-                        "compute wave], K=%d W=%d%s)",
+                        "compute wave, missing (>> 8): 1 west 2 south 4 east-LDS 8 east-grant "
+                        "16 north-grant 32 state window; 128: loader], K=%d W=%d%s)",
                         err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W,
                         c->world > 1 ? "; multi-GPU: a neighbour rank may not be running" : "");
         return fail(BURG_EHIP,
@@ -583,7 +605,7 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->comm_polls = c->eng_eff == BURG_ENGINE_PIPE ? (int64_t)ss.why[5] : 0;
         st->nonfinite_diagonals = (int64_t)ss.nonfinite_diagonals;
     }
-    if (ss.nonfinite_diagonals)
+    if (ss.nonfinite_diagonals && !std::getenv("BURG_ALLOW_NONFINITE"))  // (diagnostics knob)
         return fail(BURG_ENAN,
                     "the march produced non-finite states (NaN/Inf) on %llu diagonals: a NaN/Inf "
                     "input or a negative discriminant 0.25 + hx*Cu + hy*Cv",
@@ -1616,6 +1638,208 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
     (void)hipEventDestroy(f1);
     if (rc == BURG_OK && st && st->unconverged_steps > 0)
         return fail(BURG_ENOCONV, "%d steps hit the pass cap", st->unconverged_steps);
+    return rc;
+}
+
+// The .npy header np.save writes for a C-order float64 (m, ncols) array
+// (format 1.0: magic, version, little-endian header length, the dict padded
+// with spaces to a 64-byte boundary, newline).
+static std::string npy_header(size_t m, size_t ncols)
+{
+    std::string d = "{'descr': '<f8', 'fortran_order': False, 'shape': (" + std::to_string(m) +
+                    ", " + std::to_string(ncols) + "), }";
+    size_t total = 10 + d.size() + 1;
+    const size_t pad = (64 - total % 64) % 64;
+    d.append(pad, ' ');
+    d.push_back('\n');
+    std::string h("\x93NUMPY\x01\x00", 8);
+    const unsigned short hl = (unsigned short)d.size();
+    h.push_back((char)(hl & 0xff));
+    h.push_back((char)(hl >> 8));
+    return h + d;
+}
+
+// burg_run_npy: one trajectory, its snapshot matrix written straight into a
+// .npy file (load_or_compute_snaps' cache, C/hypernet2D.py:3141-3143).  The
+// trajectory stays in the HBM ring; row blocks of the C-order matrix are
+// gathered on the device, copied into one of two pinned host buffers and
+// written by a writer thread while the next block is gathered and copied.
+int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, const char *path,
+                 burg_stats *st)
+{
+    if (int e = check_ready(c)) return e;
+    if (st) std::memset(st, 0, sizeof *st);
+    if (!w0 || !path || !*path) return fail(BURG_EINVAL, "null w0 or path");
+    if (num_steps < 1 || snap_every < 1) return fail(BURG_EINVAL, "num_steps, snap_every >= 1");
+    if (c->engine == BURG_ENGINE_TILES) return fail(BURG_EINVAL, "burg_run_npy runs on the stream/pipe engines");
+    if (int e = stream_setup(c)) return e;
+    if (num_steps > stream_max_steps(c))
+        return fail(BURG_EINVAL, "num_steps %d exceeds one launch (%d)", num_steps, stream_max_steps(c));
+    const int W = c->sp.W;
+    const size_t m = c->m();
+    const int64_t ncols = num_steps / snap_every + 1;
+    const long long L = (long long)num_steps * W + W + 96;
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    size_t freeb = 0, totalb = 0;
+    HIPCHK(hipMemGetInfo(&freeb, &totalb));
+    const size_t need = (size_t)L * per_entry, have = c->ring_entries * sizeof(d2);
+    if (need > have && need > (freeb + have) / 100 * 85)
+        return fail(BURG_ENOMEM, "the %d-step trajectory (%.1f GB of ring) does not fit in HBM; "
+                    "use burg_run", num_steps, (double)need / 1e9);
+    if (int e = ensure_ring(c, L)) return e;
+    // row blocks: about 128 MB each (at least one row)
+    const size_t row_bytes = (size_t)ncols * sizeof(double);
+    size_t R = std::max<size_t>(1, ((size_t)128 << 20) / row_bytes);
+    if (const char *e = std::getenv("BURG_NPY_BLOCK_ROWS")) {  // test knob: force many blocks
+        const long long v = std::atoll(e);
+        if (v > 0) R = std::min(R, (size_t)v);
+    }
+    R = std::min(R, m);
+    double *d_blk = nullptr, *h_blk[2] = {nullptr, nullptr};
+    int fd = -1;
+    int rc = BURG_OK;
+    std::thread writer;
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t ready_bytes[2] = {0, 0};  // > 0: buffer i holds bytes for the writer
+    bool busy[2] = {false, false}, stop = false, werr = false;
+    auto cleanup = [&]() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        if (writer.joinable()) writer.join();
+        (void)hipStreamSynchronize(c->stream);
+        dfree(d_blk);
+        for (auto &h : h_blk)
+            if (h) (void)hipHostFree(h), h = nullptr;
+        if (fd >= 0) close(fd);
+    };
+    if ((rc = dalloc(&d_blk, 2 * R * (size_t)ncols))) return rc;
+    for (auto &h : h_blk)
+        if (hipHostMalloc((void **)&h, R * row_bytes, hipHostMallocDefault) != hipSuccess) {
+            cleanup();
+            return fail(BURG_ENOMEM, "pinned staging buffers (2 x %zu bytes)", R * row_bytes);
+        }
+    fd = open(path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
+    if (fd < 0) {
+        cleanup();
+        return fail(BURG_EINVAL, "open(%s): %s", path, strerror(errno));
+    }
+    const std::string hdr = npy_header(m, (size_t)ncols);
+    if (write(fd, hdr.data(), hdr.size()) != (ssize_t)hdr.size()) {
+        cleanup();
+        return fail(BURG_EINVAL, "write(%s): %s", path, strerror(errno));
+    }
+    writer = std::thread([&]() {
+        int i = 0;
+        for (;;) {
+            size_t nbytes = 0;
+            {
+                std::unique_lock<std::mutex> g(mu);
+                cv.wait(g, [&] { return ready_bytes[i] > 0 || stop; });
+                if (ready_bytes[i] == 0) return;
+                nbytes = ready_bytes[i];
+            }
+            const char *p = (const char *)h_blk[i];
+            size_t left = nbytes;
+            while (left > 0) {
+                const ssize_t wr = write(fd, p, left);
+                if (wr <= 0) {
+                    std::lock_guard<std::mutex> g(mu);
+                    werr = true;
+                    break;
+                }
+                p += wr;
+                left -= (size_t)wr;
+            }
+            {
+                std::lock_guard<std::mutex> g(mu);
+                ready_bytes[i] = 0;
+                busy[i] = false;
+            }
+            cv.notify_all();
+            i ^= 1;
+        }
+    });
+
+    // the trajectory: one launch, every state in the ring
+    const auto t_start = std::chrono::steady_clock::now();
+    stream_stats_begin(c);
+    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, m * sizeof(double), hipMemcpyHostToDevice,
+                          c->stream));
+    CHK(launch_ring_load(stream_args(c, L, 0, 0), W, c->d_state[c->cur], c->stream));
+    float ms = 0.f;
+    if ((rc = stream_launch(c, L, 0, num_steps, &ms))) {
+        cleanup();
+        return rc;
+    }
+    // row blocks -> pinned buffers -> file, double-buffered
+    float flush_ms = 0.f;
+    hipEvent_t f0 = nullptr, f1 = nullptr;
+    (void)hipEventCreate(&f0);
+    (void)hipEventCreate(&f1);
+    int bi = 0;
+    for (size_t e0 = 0; e0 < m && rc == BURG_OK; e0 += R, bi ^= 1) {
+        const size_t ne = std::min(R, m - e0);
+        {
+            std::unique_lock<std::mutex> g(mu);
+            cv.wait(g, [&] { return !busy[bi] || werr; });
+            if (werr) break;
+            busy[bi] = true;
+        }
+        double *dst = d_blk + (size_t)bi * R * ncols;
+        (void)hipEventRecord(f0, c->stream);
+        if (launch_ring_extract_rows(stream_args(c, L, 0, 0), W, e0, ne, 0, snap_every, (int)ncols,
+                                     dst, c->stream) ||
+            hipMemcpyAsync(h_blk[bi], dst, ne * row_bytes, hipMemcpyDeviceToHost, c->stream) !=
+                hipSuccess) {
+            rc = fail(BURG_EHIP, "snapshot row block copy failed");
+            break;
+        }
+        (void)hipEventRecord(f1, c->stream);
+        if (hipEventSynchronize(f1) != hipSuccess) {
+            rc = fail(BURG_EHIP, "snapshot row block copy failed: %s", hipGetErrorString(hipGetLastError()));
+            break;
+        }
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, f0, f1);
+        flush_ms += t;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            ready_bytes[bi] = ne * row_bytes;
+        }
+        cv.notify_all();
+    }
+    // drain the writer, then stop it
+    {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [&] { return (!busy[0] && !busy[1]) || werr; });
+    }
+    if (werr && rc == BURG_OK) rc = fail(BURG_EINVAL, "write(%s) failed", path);
+    if (rc == BURG_OK && fsync(fd) != 0) {
+        // page cache is enough for np.load; fsync failures (e.g. pipes) are not fatal
+    }
+    const double wall_ms =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    if (rc == BURG_OK) {
+        const long long o_last = 0;
+        rc = launch_ring_extract(stream_args(c, L, o_last, 0), W, num_steps, 1, 1,
+                                 c->d_state[c->cur ^ 1], 1, c->stream);
+        if (rc) rc = fail(BURG_EHIP, "ring extract launch failed");
+        else c->cur ^= 1;
+    }
+    if (rc == BURG_OK) rc = stream_stats_end(c, st, num_steps, 1);
+    if (st) {
+        st->loop_ms = ms;
+        st->flush_ms = flush_ms;
+        st->march_kernel_ms = wall_ms;  // whole call (trajectory + write), wall clock
+        st->march_launches = 1;
+    }
+    (void)hipEventDestroy(f0);
+    (void)hipEventDestroy(f1);
+    cleanup();
     return rc;
 }
 

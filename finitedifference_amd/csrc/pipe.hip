@@ -27,10 +27,16 @@
 //     in LDS (st[W][64]): no global load at all in the loop;
 //   * wide tiles (W = 32 .. 1024, the 4096^2 grid and the multi-GPU slabs of
 //     2048 x 8192 / 16384 cells): the tile's trajectory ring in HBM, entry
-//     s - W (written by the same wave W diagonals earlier: same-wave program
-//     order), prefetched kPf diagonals ahead into registers -- one coalesced
-//     1 KB load per diagonal.  Its s_waitcnt waits only for memory operations
-//     at least kPf diagonals old (vmcnt counts loads and stores in issue order).
+//     s - W (written by the same wave W diagonals earlier).  A sixth wave per
+//     workgroup, the loader, streams those entries into an LDS window of kWin
+//     diagonals per compute wave (LDS-DMA, one 1 KB row per diagonal) and
+//     publishes how far each window is filled; the compute waves read LDS
+//     only.  A compute wave never issues a global load, so no s_waitcnt of
+//     its own ever waits on its stores (vmcnt counts loads and stores
+//     together, in issue order).  The loader reads an entry only after the
+//     compute wave has published that the entry's store completed: at the
+//     start of each block of U diagonals it waits vmcnt(3U) -- every store
+//     older than U diagonals -- and publishes that point.
 //
 // South/north streams are indexed by diagonal: comm lane j of wave k's group
 // of 16 handles the diagonals d = j (mod 16) of that tile -- the granule of
@@ -75,11 +81,13 @@ constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, s
 constexpr int kR = kPipeR;
 constexpr int kRL = kPipeRL;
 constexpr unsigned G = kGranuleStride;
-constexpr int kThreads = 5 * kWave;
+template <int W>
+constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
 constexpr int kNI = 64;   // south inbox ring (diagonals), power of two
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
 constexpr int kLA = 16;   // poll window (diagonals ahead of a compute wave's progress)
-constexpr int kPf = 8;    // wide tiles: prefetch distance of the previous state (diagonals)
+constexpr int kWin = 16;  // wide tiles: LDS window of previous states per compute wave (diagonals)
+constexpr int kUw = 8;    // wide tiles: diagonals per block (progress / store completion published)
 
 __device__ __forceinline__ d2 as_d2(v4u v)
 {
@@ -202,6 +210,9 @@ template <int W, bool SWEEP>
 struct PipeLds {
     static constexpr bool WIDE = is_wide<W>();
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
+    // wide: previous states by diagonal, filled by LDS-DMA -- first in the
+    // image: the DMA's LDS address comes from M0[15:0] (the 64 KB below 2^16)
+    v4u win[4][WIDE ? kWin : 1][WIDE ? kWave : 1];
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
@@ -214,17 +225,22 @@ struct PipeLds {
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
+    int done[4];            // wide: per compute wave, diagonals whose stores completed
+    int filled[4];          // wide: per compute wave, window filled below this diagonal
 };
 
 template <int W, bool SWEEP>
-__global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
+__global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 {
+    constexpr int kThreads = threads_of<W>();
+    static_assert(!is_wide<W>() || sizeof(PipeLds<W, SWEEP>::win) <= 65536,
+                  "LDS-DMA window must sit below 64 KB");
     constexpr bool WIDE = is_wide<W>();
     static_assert(W == 8 || W == 16 || (WIDE && W <= 1024 && (W & (W - 1)) == 0),
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
-    constexpr int U = WIDE ? kPf : 4;  // diagonals per block (progress published per block)
+    constexpr int U = WIDE ? kUw : 4;  // diagonals per block (progress published per block)
     __shared__ PipeLds<W, SWEEP> sm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -280,7 +296,11 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     for (int i = threadIdx.x; i < kRL * kWave; i += kThreads) (&sm.inw[0][0])[i] = lds_empty_g();
     for (int i = threadIdx.x; i < 4 * kNI; i += kThreads) (&sm.ins[0][0])[i] = lds_empty_g();
     if (threadIdx.x < 6) sm.perm[threadIdx.x] = 0;
-    if (threadIdx.x < 4) sm.prog[threadIdx.x] = 0;
+    if (threadIdx.x < 4) {
+        sm.prog[threadIdx.x] = 0;
+        sm.done[threadIdx.x] = 0;
+        sm.filled[threadIdx.x] = 0;
+    }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
@@ -440,6 +460,85 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         if (lane == 0) atomicAdd(&a.stats->why[5], iters);
         return;
     }
+    if (WIDE && wave == 5) {
+        // ================= loader wave (wide tiles) =================
+        // window slot d mod kWin of compute wave k <- ring entry (origin +
+        // d - W) of its tile, once (1) the slot's previous diagonal is done
+        // (d < prog + kWin), (2) that entry's store has completed
+        // (d - W < done) -- entries d < W are the initial state, written
+        // before the launch.
+        __builtin_amdgcn_s_setprio(0);
+        // the compute waves run whole blocks of U diagonals
+        const int total = (KW + kWave - 1 + U - 1) / U * U;
+        const long long L = a.L;
+        int nf[4] = {0, 0, 0, 0};
+        long long t_prog = now_rt();
+        for (;;) {
+            bool left = false, issued = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (k >= nval) continue;
+                const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
+                const int lim = min(min(total, pk + kWin), dk + W);
+                if (nf[k] < lim) {
+                    const __amdgpu_buffer_rsrc_t ring =
+                        rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * L * kWave, (size_t)L * kWave * 16);
+                    long long e = (a.origin + nf[k] - W) % L;
+                    e = e < 0 ? e + L : e;
+                    if (a.dbg & 2) {
+                        // diagnostics: register staging instead of LDS-DMA
+                        for (; nf[k] < lim; ++nf[k]) {
+                            const v4u x = __builtin_amdgcn_raw_buffer_load_b128(
+                                ring, (unsigned)e * 1024u + lane * 16u, 0, 16);
+                            lds_st(&sm.win[k][nf[k] & (kWin - 1)][lane], x);
+                            e = e + 1 == L ? 0 : e + 1;
+                        }
+                    } else {
+                        for (; nf[k] < lim; ++nf[k]) {
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                                ring, (__attribute__((address_space(3))) void *)&sm.win[k][nf[k] & (kWin - 1)][0],
+                                16, (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
+                            e = e + 1 == L ? 0 : e + 1;
+                        }
+                    }
+                    issued = true;
+                }
+                left |= nf[k] < total;
+            }
+            if (issued) {
+                __builtin_amdgcn_s_waitcnt(0);  // the DMA rows have landed in LDS
+                if ((a.dbg & 4) && a.dbgbuf && wg == 0 && lane == 0 && lds_ldi(&sm.filled[0]) == 0) {
+                    const d2 w0v = as_d2(lds_ld(&sm.win[0][0][0]));
+                    long long e0 = (a.origin - W) % L;
+                    e0 = e0 < 0 ? e0 + L : e0;
+                    const d2 g0 = a.ring[(size_t)e0 * kWave];
+                    const double v[8] = {w0v.x, w0v.y, g0.x, g0.y, (double)e0, (double)L,
+                                         (double)a.origin, (double)nf[0]};
+                    for (int i = 0; i < 8; ++i) a.dbgbuf[16 + i] = v[i];
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (k < nval && lane == 0) lds_sti(&sm.filled[k], nf[k]);
+                t_prog = now_rt();
+            }
+            if (!left || lds_ldi(&sm.perm[5])) break;
+            if (!issued) {
+                if (now_rt() - t_prog > a.spin_ticks) {
+                    if (lane == 0 && !lds_ldi(&sm.perm[5])) {
+                        lds_sti(&sm.perm[5], 1);
+                        if (atomicOr(a.err, 1u) == 0) {
+                            a.err[1] = (unsigned)(ti * ntj + tj0);
+                            a.err[2] = (unsigned)nf[0];
+                            a.err[3] = 128u;
+                        }
+                    }
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        return;
+    }
     if (wave >= nval) return;
 
     // ================= compute wave =================
@@ -491,24 +590,11 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0;
     bool aborted = false;
 
-    // wide tiles: the previous state of diagonal s (ring entry s - W), kPf
-    // diagonals ahead; pr = ring entry of the next prefetch
-    v4u pf[WIDE ? kPf : 1];
-    long long pr = 0;
-    if constexpr (WIDE) {
-        pr = (a.origin - W) % L;
-        pr = pr < 0 ? pr + L : pr;
-#pragma unroll
-        for (int i = 0; i < kPf; ++i) {
-            pf[i] = ld_plain(ring, (unsigned)pr * 1024u + lane16);
-            pr = pr + 1 == L ? 0 : pr + 1;
-        }
-    }
 
     // LDS inputs of diagonal s, read at the end of diagonal s - 1
     struct In {
         v4u xs, cs, gw, gs;
-        int pn, pe;
+        int pn, pe, pf;
         unsigned ee;
         bool nt;     // sweep: first step of the lane's next trajectory (state reset)
         double src;  // sweep: the column's source term of the step's trajectory
@@ -529,8 +615,12 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             in.xs = my_st[(s & (W - 1)) * kWave + lane];
             in.src = 0.0;
         } else {
+            // wide: the window's fill mark first, then the slot (LDS reads of
+            // one wave complete in order)
             in.nt = false;
             in.src = 0.0;
+            in.pf = lds_ldi(&sm.filled[k]);
+            in.xs = lds_ld(&sm.win[k][s & (kWin - 1)][lane]);
         }
         in.cs = sm.cc[k][c];
         in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
@@ -542,7 +632,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     };
 
     // one diagonal; returns false when the launch is aborted
-    auto diagonal = [&](const int s, const int u, In &in) -> bool {
+    auto diagonal = [&](const int s, In &in) -> bool {
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -553,22 +643,26 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         const bool out_e = atE && valid && rowok;
         const bool out_n = lane == top && valid && has_north;
         // ---- inflow-independent part of the cell (MarchCell::pre, same op order)
-        const d2 x = as_d2(WIDE ? pf[u % (WIDE ? kPf : 1)] : in.xs);
-        const d2 co = as_d2(in.cs);
-        const double pu = x.x, pv = x.y;
-        const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
         const double lbu = SWEEP && in.nt ? lb_next : lb;
-        const double srcc = SWEEP ? in.src : co.y;
-        const double sl = (col0_tile && at0) ? srcc + lbu : srcc;
-        MarchCell::Pre p;
-        p.hx = hx;
-        const double hu = 0.5 * pu;
-        p.xfp = ax * (hu * pu);
-        p.xhp = ax * (hu * pv);
-        p.yhp = ay * (hu * pv);
-        p.ygp = ay * ((0.5 * pv) * pv);
-        p.bu = ((pu - p.xfp) - p.yhp) + sl;
-        p.bv = (pv - p.ygp) - p.xhp;
+        auto pre_of = [&](const In &v) -> MarchCell::Pre {
+            const d2 x = as_d2(v.xs);
+            const d2 co = as_d2(v.cs);
+            const double pu = x.x, pv = x.y;
+            const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
+            const double srcc = SWEEP ? v.src : co.y;
+            const double sl = (col0_tile && at0) ? srcc + lbu : srcc;
+            MarchCell::Pre q;
+            q.hx = hx;
+            const double hu = 0.5 * pu;
+            q.xfp = ax * (hu * pu);
+            q.xhp = ax * (hu * pv);
+            q.yhp = ay * (hu * pv);
+            q.ygp = ay * ((0.5 * pv) * pv);
+            q.bu = ((pu - q.xfp) - q.yhp) + sl;
+            q.bv = (pv - q.ygp) - q.xhp;
+            return q;
+        };
+        MarchCell::Pre p = pre_of(in);
         const MarchCell::Row rw{ay, hy, lbu};
         // ---- wait until inputs are deposited and outbound slots are granted
         auto blocked = [&](const In &v) -> bool {
@@ -576,6 +670,7 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
             b |= east_lds && out_e && v.ee != kLdsEmptyHi;
             b |= east_glob && out_e && q >= v.pe;
             b |= out_n && t >= v.pn;
+            if constexpr (WIDE) b |= s >= v.pf;
             return b;
         };
         if (__builtin_expect(__any(blocked(in)), 0)) {
@@ -587,16 +682,41 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
                 in = fetch(s);
                 if (!__any(blocked(in))) break;
                 if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
+                    // which input / grant was missing (diagnosis in err[3] >> 8)
+                    unsigned why = 0;
+                    why |= __any(need_w && !l_is_data(in.gw)) ? 1u : 0u;
+                    why |= __any(lane == 0 && need_s && !l_is_data(in.gs)) ? 2u : 0u;
+                    why |= __any(east_lds && out_e && in.ee != kLdsEmptyHi) ? 4u : 0u;
+                    why |= __any(east_glob && out_e && q >= in.pe) ? 8u : 0u;
+                    why |= __any(out_n && t >= in.pn) ? 16u : 0u;
+                    if (WIDE && s >= in.pf) why |= 32u;
                     if (lane == 0 && !lds_ldi(&sm.perm[5])) {
                         lds_sti(&sm.perm[5], 1);
                         if (atomicOr(a.err, 1u) == 0) {
                             a.err[1] = (unsigned)tile;
                             a.err[2] = (unsigned)s;
-                            a.err[3] = 32u;
+                            a.err[3] = 32u | (why << 8);
                         }
                     }
                     return false;
                 }
+            }
+            // wide tiles: the previous state arrives with the window fill
+            if constexpr (WIDE) p = pre_of(in);
+        }
+        if (WIDE && (a.dbg & 1)) {
+            // diagnostics: the window row must equal the ring entry it copies
+            long long e = (a.origin + s - W) % L;
+            e = e < 0 ? e + L : e;
+            const v4u r0 = ld_plain(ring, (unsigned)e * 1024u + lane16);
+            const bool bad = valid && rowok && (r0.x != in.xs.x || r0.y != in.xs.y ||
+                                                r0.z != in.xs.z || r0.w != in.xs.w);
+            // lanes whose window row differs from the ring: [0] initial state, [1] later steps
+            const unsigned long long b0 = __ballot(bad && t < W), b1 = __ballot(bad && t >= W);
+            if (lane == 0) {
+                if (b0) atomicAdd(&a.stats->why[0], (unsigned long long)__popcll(b0));
+                if (b1) atomicAdd(&a.stats->why[1], (unsigned long long)__popcll(b1));
+                if (b0 | b1) atomicAdd(&a.stats->why[2], 1ull);
             }
         }
         // ---- the cell's chain
@@ -611,6 +731,12 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         double oe0, oe1, on0, on1, o0, o1;
         bool ok;
         MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
+        if ((a.dbg & 4) && tile == 0 && lane == 0 && s == 0 && a.dbgbuf) {
+            const d2 xx = as_d2(in.xs);
+            const double v[16] = {xx.x, xx.y, p.hx, as_d2(in.cs).y, 0.0, ay, lbu, e0, e1, n0, n1,
+                                  o0, o1, p.bu, p.bv, (double)ok};
+            for (int i = 0; i < 16; ++i) a.dbgbuf[i] = v[i];
+        }
         if (__builtin_expect(__any(!ok && valid && rowok), 0)) {
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             ++ieee_n;
@@ -628,7 +754,11 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
         if constexpr (!WIDE) {
             if (t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
         }
-        st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
+        // wide tiles: the loader wave reads this entry back (sc1 DMA) W
+        // diagonals later, so it is stored write-through to L2 (sc1): the
+        // store's vmcnt then completes at L2, which the done[] protocol needs
+        if constexpr (WIDE) st_dev(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
+        else st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
         pw = pw + 1 == L ? 0 : pw + 1;
         const v4u eo = as_v4u(oe0, oe1);
         const int aq = a.qbase + q;
@@ -660,10 +790,6 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
-        if constexpr (WIDE) {
-            pf[u % (WIDE ? kPf : 1)] = ld_plain(ring, (unsigned)pr * 1024u + lane16);
-            pr = pr + 1 == L ? 0 : pr + 1;
-        }
         in = fetch(s + 1);
         return true;
     };
@@ -675,10 +801,18 @@ __global__ __launch_bounds__(kThreads) void pipe_kernel(PipeArgs a)
     // in flight -- into every diagonal.
     __builtin_amdgcn_s_waitcnt(0);
     for (int sb = 0; sb < total && !aborted; sb += U) {
+        if constexpr (WIDE) {
+            // every store older than this block's predecessor has completed
+            // (at most 3 stores per diagonal, no loads): the loader may read
+            // ring entries written before diagonal sb - U
+            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            static_assert(3 * kUw == 24, "vmcnt covers one block of stores");
+            if (lane == 0) lds_sti(&sm.done[k], sb - U);
+        }
         if (lane == 0) lds_sti(&sm.prog[k], sb);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            if (!aborted && !diagonal(sb + u, u, in)) aborted = true;
+            if (!aborted && !diagonal(sb + u, in)) aborted = true;
         }
     }
     if (lane == 0) {
@@ -762,7 +896,9 @@ int pipe_max_resident_blocks(int W, bool sweep)
     const void *fn = pipe_fn(W, sweep);
     if (!fn) return -1;
     const size_t dyn = pipe_dyn_lds(W, fn, pipe_per_cu_opt());
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kThreads, dyn) != hipSuccess) return -3;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
+        hipSuccess)
+        return -3;
     return n * ncu;
 }
 
@@ -778,7 +914,8 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;
     PipeArgs args = a;
     void *kargs[] = {&args};
-    if (hipLaunchKernel(fn, dim3(blocks), dim3(kThreads), kargs, dyn, st) != hipSuccess) return -3;
+    const int threads = W > 16 ? 6 * kWave : 5 * kWave;
+    if (hipLaunchKernel(fn, dim3(blocks), dim3(threads), kargs, dyn, st) != hipSuccess) return -3;
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

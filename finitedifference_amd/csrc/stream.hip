@@ -463,6 +463,31 @@ __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int 
     out[(n + cell) * ldo + j] = v.y;
 }
 
+// Row block of the C-order snapshot matrix: out[(e - e0) * ncols + j] =
+// element e (u plane, then v plane) of state k0 + j*kstep, e in [e0, e0 + ne).
+// Consecutive threads walk j: the reads gather 16-B cells from the ring, the
+// writes are the contiguous rows of the .npy file.
+__global__ void ring_extract_rows_kernel(StreamArgs a, int W, size_t e0, size_t ne, int k0,
+                                         int kstep, int ncols, double *out)
+{
+    const size_t n = (size_t)a.cf.nx * a.cf.ny;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= ne * (size_t)ncols) return;
+    const size_t er = idx / ncols;
+    const int j = (int)(idx - er * ncols);
+    const size_t e = e0 + er;
+    const bool vplane = e >= n;
+    const size_t cell = vplane ? e - n : e;
+    const int row = (int)(cell / a.cf.nx), col = (int)(cell - (size_t)row * a.cf.nx);
+    const int ti = row / kWave, lane = row - ti * kWave;
+    const int tj = col / W, cl = col - tj * W;
+    const int tile = ti * a.ntj + tj;
+    const d2 v = a.ring[((size_t)tile * a.L + ring_entry(a.origin, a.L, W, k0 + j * kstep, cl, lane)) *
+                            kWave +
+                        lane];
+    out[idx] = vplane ? v.y : v.x;
+}
+
 template <int W, int D, int DM = 4>
 int launch_w(const StreamArgs &a, int blocks, hipStream_t st)
 {
@@ -577,6 +602,16 @@ int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st
     const size_t total = (size_t)a.ntiles * kWave * W;
     hipLaunchKernelGGL(ring_load_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        a, W, w);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int launch_ring_extract_rows(const StreamArgs &a, int W, size_t e0, size_t ne, int k0, int kstep,
+                             int ncols, double *out, hipStream_t st)
+{
+    const size_t total = ne * (size_t)ncols;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(ring_extract_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       st, a, W, e0, ne, k0, kstep, ncols, out);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -8,6 +8,8 @@ reference module ``hypernet2D`` for the FOM path (paths relative to
   make_ddx / get_ops            C/hypernet2D.py:2410-2416, 2433-2444 (scipy setup)
   inviscid_burgers_implicit2D   C/hypernet2D.py:72-131     -> burg_run (HIP)
   inviscid_burgers_res2D_alt    C/hypernet2D.py:2512-2570  -> burg_residual (HIP)
+  inviscid_burgers_res2D        C/hypernet2D.py:2468-2510  -> burg_residual (HIP)
+  plot_snaps                    C/hypernet2D.py:3147-3180  (matplotlib, host)
   inviscid_burgers_exact_jac2D  C/hypernet2D.py:2627-2656  -> JacobianOperator
                                 (burg_jvp / burg_block_solve, HIP)
   newton_raphson                C/hypernet2D.py:1811-1857  (host control loop)
@@ -79,9 +81,11 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     selects the per-step block-Jacobi tile engine, tuned by tile_w / tol /
     par_passes); solver="newton" runs the reference algorithm
     (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
-    Both return the reference's snapshot matrix.  verbose=1 prints the
-    reference's header line; verbose=2 also the per-step lines
-    (" ... Working on timestep i" and Newton's "k: rel").  out: an existing
+    Both return the reference's snapshot matrix.  verbose=1 (default) prints
+    what the reference prints: the header line, then per step
+    " ... Working on timestep i" (C/hypernet2D.py:122) and, for the newton
+    solver, Newton's "k: rel" line (:1844) -- after the run, since the whole
+    time loop is one launch; verbose=0 prints nothing.  out: an existing
     (2n, num_steps//snap_every + 1) C-contiguous float64 array (e.g. a .npy
     memmap) the snapshots are written into and returned.
     """
@@ -92,11 +96,14 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
                                      solver, newton_max_its, newton_rtol, int(snap_every),
                                      out=out)
-    if verbose >= 2:
+    if verbose:
+        lines = []
         for i in range(int(num_steps)):
-            print(" ... Working on timestep {}".format(i))
+            lines.append(" ... Working on timestep {}".format(i))
             if solver == "newton":
-                print("{}: {:3.2e}".format(its[i], rel[i]))
+                lines.append("{}: {:3.2e}".format(its[i], rel[i]))
+        if lines:
+            print("\n".join(lines))
     if return_stats:
         stats = dict(stats, step_iters=its, step_rel=rel)
         return snaps, stats
@@ -132,6 +139,16 @@ def inviscid_burgers_res2D_alt(w, grid_x, grid_y, dt, wp, mu, JDxec=None, JDyec=
     ctx = _ctx_for(grid_x, grid_y, dt, mu, device)
     r, _ = ctx.residual(w, wp)
     return r
+
+
+def inviscid_burgers_res2D(w, grid_x, grid_y, dt, wp, mu, Dxec=None, Dyec=None, *, device=0):
+    """The same residual through the reference's 1-D operators
+    (C/hypernet2D.py:2468-2510), the callback the ECSW / LSPG drivers pass
+    around (C/run_HPROM_ecsw_joshua_.py:19-21,83).  Computed on the GPU by the
+    res2D_alt stencil: the two reference forms differ only in the order of
+    the per-cell sums (<= 4.4e-16 relative).
+    Dxec/Dyec are accepted for signature compatibility and ignored."""
+    return inviscid_burgers_res2D_alt(w, grid_x, grid_y, dt, wp, mu, device=device)
 
 
 class JacobianOperator(LinearOperator):
@@ -282,10 +299,14 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
             rng = np.random.RandomState(random_state)
         else:
             rng = random_state
-        nrand = min(k + 10, ns)
+        # sklearn draws the full (ns, k + 10) Gaussian test matrix whatever k
+        # is; draw exactly that, so later draws from the same RNG match the
+        # reference run, and keep at most ns columns (they already span the
+        # whole column space of S)
         n_iter = 7 if k < 0.1 * min(m, ns) else 4
-        omega = rng.normal(size=(ns, nrand))
-        omega_cm = np.ascontiguousarray(omega.T)  # column-major (ns x nrand)
+        omega = rng.normal(size=(ns, k + 10))
+        nrand = min(k + 10, ns)
+        omega_cm = np.ascontiguousarray(omega[:, :nrand].T)  # column-major (ns x nrand)
         _lib.check(L.burg_pod_rsvd(int(device), m, ns, _lib.dptr(S), k, nrand, n_iter,
                                    _lib.dptr(omega_cm), _lib.dptr(u), _lib.dptr(sv),
                                    ctypes.byref(ms)))
@@ -298,6 +319,37 @@ def compute_error(rom_snaps, hdm_snaps):
     sq_err = np.sqrt(np.square(rom_snaps - hdm_snaps).sum(axis=0))
     rel_err = sq_err / sq_hdm
     return rel_err, rel_err.mean()
+
+
+def plot_snaps(grid_x, grid_y, snaps, snaps_to_plot, linewidth=2, color="black",
+               linestyle="solid", label=None, fig_ax=None):
+    """Mid-line slices of u for the snapshot columns in snaps_to_plot
+    (C/hypernet2D.py:3147-3180, the figures the author pickled): axis 1 shows
+    u along the middle row y = y[ny // 2], axis 2 along the middle column
+    x = x[nx // 2]; only the first line of a call carries `label`.  Returns
+    (fig, ax1, ax2); pass them back as fig_ax to overlay further calls."""
+    import matplotlib.pyplot as plt
+    if fig_ax is None:
+        fig, (ax1, ax2) = plt.subplots(2, 1)
+    else:
+        fig, ax1, ax2 = fig_ax
+    gx, gy = np.asarray(grid_x), np.asarray(grid_y)
+    xc, yc = 0.5 * (gx[1:] + gx[:-1]), 0.5 * (gy[1:] + gy[:-1])
+    jx, jy = xc.size // 2, yc.size // 2
+    n = xc.size * yc.size
+    for k, col in enumerate(snaps_to_plot):
+        u = np.asarray(snaps[:n, col]).reshape(yc.size, xc.size)
+        lab = label if k == 0 else None
+        style = dict(color=color, linestyle=linestyle, linewidth=linewidth, label=lab)
+        ax1.plot(xc, u[jy, :], **style)
+        ax1.set_xlabel("$x$")
+        ax1.set_ylabel("$u_x(x,y={:0.1f})$".format(yc[jy]))
+        ax1.grid()
+        ax2.plot(yc, u[:, jx], **style)
+        ax2.set_xlabel("$y$")
+        ax2.set_ylabel("$u_x(x={:0.1f},y)$".format(xc[jx]))
+        ax2.grid()
+    return fig, ax1, ax2
 
 
 def param_to_snap_fn(mu, snap_folder="param_snaps", suffix=".npy"):
@@ -331,7 +383,7 @@ def _commit_cache(tmp, fn, mm):
 
 
 def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="param_snaps",
-                          stream=False, mmap=False, **solver_kw):
+                          stream=False, mmap=False, direct=False, **solver_kw):
     """Load cached snapshots for mu, or compute and cache them
     (C/hypernet2D.py:3111-3145; same file names and .npy format, so caches
     are interchangeable with the reference's).  solver_kw go to
@@ -347,22 +399,46 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
     0.29 s default vs 0.52 s streamed -- file-backed pages cannot be pinned,
     so the streamed D2H runs at pageable speed.
     mmap=True on a cache hit: np.load(..., mmap_mode='r') instead of reading
-    the whole file."""
+    the whole file.  direct=True (march solver): the library writes the cache
+    file itself (burg_run_npy: the trajectory stays in HBM, row blocks of the
+    C-order matrix go through two pinned buffers to a writer thread), then
+    the file is loaded (mmap=True: mapped)."""
     if not os.path.exists(snap_folder):
         os.makedirs(snap_folder)
-    snap_fn = param_to_snap_fn(mu, snap_folder=snap_folder)
+    every = int(solver_kw.get("snap_every", 1))
+    ncols = int(num_steps) // every + 1
+    # a thinned matrix (snap_every > 1) must never pass for the reference's
+    # per-step cache: it gets a name of its own
+    snap_fn = param_to_snap_fn(mu, snap_folder=snap_folder,
+                               suffix=".npy" if every == 1 else f"+every{every}.npy")
     if snap_fn in get_saved_params(snap_folder=snap_folder):
-        print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
-        return np.load(snap_fn, mmap_mode="r" if mmap else None)[:, :num_steps + 1]
+        cached = np.load(snap_fn, mmap_mode="r")
+        if cached.shape[1] >= ncols:
+            print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
+            return cached[:, :ncols] if mmap else np.array(cached[:, :ncols])
+        print(f"Saved snaps for mu1={mu[0]}, mu2={mu[1]} hold {cached.shape[1]} of the "
+              f"{ncols} columns asked for: recomputing")
+        del cached
     print(f"Computing new snaps for mu1={mu[0]}, mu2={mu[1]}")
     t0 = time.time()
+    if direct:
+        if solver_kw.get("solver", "march") != "march":
+            raise ValueError("direct=True writes march trajectories")
+        device = solver_kw.get("device", 0)
+        ctx = _ctx_for(grid_x, grid_y, dt, mu, device, solver_kw.get("allow_nonsquare", False),
+                       engine=solver_kw.get("engine", "pipe"))
+        tmp = snap_fn + ".partial.npy"
+        ctx.run_to_npy(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), tmp,
+                       snap_every=every)
+        os.replace(tmp, snap_fn)
+        print("Elapsed time: {:3.3e}".format(time.time() - t0))
+        return np.load(snap_fn, mmap_mode="r" if mmap else None)
     if not stream:
         snaps = inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, **solver_kw)
         print("Elapsed time: {:3.3e}".format(time.time() - t0))
         np.save(snap_fn, snaps)
         return snaps
     m = np.asarray(w0).size
-    ncols = int(num_steps) // int(solver_kw.get("snap_every", 1)) + 1
     tmp, mm = _open_cache(snap_fn, m, ncols)
     inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, out=mm, **solver_kw)
     print("Elapsed time: {:3.3e}".format(time.time() - t0))

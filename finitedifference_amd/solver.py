@@ -143,6 +143,16 @@ class FOMContext:
             warnings.warn(self._L.burg_last_error().decode(), _lib.NotConvergedWarning)
         return snaps, st.as_dict(), its, rel
 
+    def run_to_npy(self, w0, num_steps, path, snap_every=1):
+        """One trajectory written straight into the .npy file `path`
+        (burg_run_npy: pinned double-buffered writer); returns stats
+        (loop_ms launch, flush_ms gathers + D2H, march_kernel_ms whole call)."""
+        w0 = self._vec(w0, "w0")
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_run_npy(self._h, _lib.dptr(w0), int(num_steps), int(snap_every),
+                                        str(path).encode(), ctypes.byref(st)))
+        return st.as_dict()
+
     def upload(self, w):
         w = self._vec(w, "w")
         _lib.check(self._L.burg_upload_state(self._h, _lib.dptr(w)))

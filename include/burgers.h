@@ -15,6 +15,8 @@
  *                       (+ np.linalg.norm of it, :1831/:1839)
  *   burg_jvp            C/hypernet2D.py:2627-2656 inviscid_burgers_exact_jac2D(w) @ x
  *   burg_block_solve    C/hypernet2D.py:1854      spsolve(J(w), rhs)
+ *   burg_run_npy        C/hypernet2D.py:3141-3143  inviscid_burgers_implicit2D + np.save
+ *                       of the snapshot cache (load_or_compute_snaps)
  *   burg_sweep          a loop of inviscid_burgers_implicit2D over a mu set
  *                       (C/run_prom.py:59-71, C/run_tests.py:38-49)
  *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
@@ -215,6 +217,18 @@ int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *
  * trajectory's final state becomes the resident state.  Pipe engine only. */
 int burg_sweep(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b, int num_steps,
                double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *stats);
+
+/* One trajectory straight into a snapshot-cache file (load_or_compute_snaps'
+ * compute-then-np.save, C/hypernet2D.py:3141-3143): the
+ * march runs in one launch with every state kept in HBM, then the C-order
+ * (2n x num_steps/snap_every+1) snapshot matrix is written to `path` in
+ * np.save's .npy format, row blocks gathered on the device and copied into
+ * two pinned host buffers that a writer thread drains while the next block
+ * is copied.  stats: loop_ms = launch time, flush_ms = device time of the
+ * gathers + D2H copies, march_kernel_ms = wall time of the whole call.
+ * Single-trajectory rings only (BURG_ENOMEM when it does not fit in HBM). */
+int burg_run_npy(burg_ctx *ctx, const double *w0, int num_steps, int snap_every, const char *path,
+                 burg_stats *stats);
 
 /* ECSW hyper-reduction training matrix (compute_ECSW_training_matrix_2D,
  * C/hypernet2D.py:2719-2740), with the context's problem (grid, dt, mu of

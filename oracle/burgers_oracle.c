@@ -39,6 +39,9 @@
  * and is restated here op-for-op as the bitwise checker of the HIP march.
  */
 #include <math.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -271,6 +274,41 @@ void orc_march_step(int nx, int ny, const double *inv_dx, const double *inv_dy,
     }
     free(yh);
     free(yg);
+}
+
+/* ------------------------------------------------------------------------ */
+/* CPU baseline (bench.py's cpu_baseline leg, not a parity checker): the
+ * reference's snapshot generation over a mu set (C/run_prom.py:59-71 calls
+ * load_or_compute_snaps once per mu) with the march above, one trajectory per
+ * OpenMP thread -- the independent work the reference leaves on the table.
+ * src_b[j*nx + c], lbc_b[j*ny + r]: trajectory j's coefficients; every
+ * trajectory starts from w0 and runs num_steps steps (states ping-ponged, not
+ * kept).  Returns the threads used.                                          */
+int orc_march_sweep(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                    const double *src_b, const double *lbc_b, double dt, const double *w0,
+                    int nmu, int num_steps, int threads)
+{
+    const size_t m = 2 * (size_t)nx * ny;
+    int used = 1;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(threads)
+    for (int j = 0; j < nmu; ++j) {
+#ifdef _OPENMP
+        if (j == 0) used = omp_get_num_threads();
+#endif
+        double *a = (double *)malloc(m * sizeof(double));
+        double *b = (double *)malloc(m * sizeof(double));
+        memcpy(a, w0, m * sizeof(double));
+        for (int i = 0; i < num_steps; ++i) {
+            orc_march_step(nx, ny, inv_dx, inv_dy, src_b + (size_t)j * nx, lbc_b + (size_t)j * ny,
+                           dt, a, b);
+            double *t = a;
+            a = b;
+            b = t;
+        }
+        free(a);
+        free(b);
+    }
+    return used;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -115,6 +115,22 @@ class Problem:
                                     _p(w), max_its, ctypes.c_double(cutoff), ctypes.byref(rel))
         return w, its, rel.value
 
+    def march_sweep(self, w0, mus, num_steps, threads):
+        """CPU baseline: one march trajectory per mu (same grid and dt), one
+        OpenMP thread each (orc_march_sweep); returns the threads used."""
+        srcs, lbcs = [], []
+        for mu in mus:
+            q = Problem(self.nx, self.ny, self.dt, mu, Ly=self.grid_y[-1],
+                        allow_nonsquare=self.nx != self.ny)
+            srcs.append(q.src)
+            lbcs.append(q.lbc)
+        src_b = np.ascontiguousarray(np.stack(srcs))
+        lbc_b = np.ascontiguousarray(np.stack(lbcs))
+        return lib().orc_march_sweep(self.nx, self.ny, _p(self.inv_dx), _p(self.inv_dy),
+                                     _p(src_b), _p(lbc_b), ctypes.c_double(self.dt),
+                                     _p(np.ascontiguousarray(w0, dtype=np.float64)), len(mus),
+                                     int(num_steps), int(threads))
+
     def fom(self, w0, num_steps, solver="march", max_its=100, cutoff=1e-12):
         """Step-major trajectory (num_steps+1, m) + Newton counts/rels."""
         snaps = np.empty((num_steps + 1, self.m))

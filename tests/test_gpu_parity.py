@@ -864,3 +864,119 @@ def test_lspg_solve_kernel_path(gpu, monkeypatch):
     with pytest.raises(_lib.BurgersError):
         H.inviscid_burgers_implicit2D_LSPG(gx, gy, np.ones(2 * N * N), dt, 1, (m1, m2),
                                            np.hstack([B[:, :3], B[:, :1]]), verbose=False)
+
+
+# ------------------------------------------------- drop-in host surface --
+def test_run_fom_main_dropin(gpu, tmp_path, monkeypatch, capsys):
+    """run_fom.main (C/run_fom.py:9-52) end to end in a scratch cwd: the
+    cache file and the hdm_snaps file carry the reference's names, the
+    trajectory is the reference's (ref_small n50: 50^2, 20 steps, mu =
+    (4.75, 0.02)), the per-step lines of C/hypernet2D.py:122 are printed, and
+    a second call is served from the cache."""
+    from finitedifference_amd import run_fom
+    g = golden("ref_small.npz")
+    monkeypatch.chdir(tmp_path)
+    el, snaps = run_fom.main(4.75, 0.02, num_cells=50, num_steps=20)
+    out = capsys.readouterr().out
+    assert " ... Working on timestep 19" in out and "Computing new snaps" in out
+    assert os.path.exists("param_snaps/mu1_4.75+mu2_0.02.npy")
+    assert os.path.exists("hdm_snaps_mu1_4.75_mu2_0.020.npy")
+    ref = g["n50_snaps"]
+    assert snaps.shape == ref.shape
+    assert max(rel(snaps[:, j], ref[:, j]) for j in range(1, 21)) <= REF_TOL
+    el2, snaps2 = run_fom.main(4.75, 0.02, num_cells=50, num_steps=20)
+    assert "Loading saved snaps" in capsys.readouterr().out
+    assert np.array_equal(snaps2, snaps)
+    assert np.array_equal(np.load("hdm_snaps_mu1_4.75_mu2_0.020.npy"), snaps)
+
+
+@pytest.mark.parametrize("N", [16, 64])
+def test_reference_residual_jacobian_newton_api(gpu, N):
+    """The reference's operator-level API (drop-in names): res2D_alt and
+    res2D (C/hypernet2D.py:2512,2468), exact_jac2D(w) @ x (:2627) with the
+    operators the reference builds (get_ops), and newton_raphson (:1811) with
+    the JacobianOperator -- against the reference's own outputs (ref_ops)."""
+    from finitedifference_amd import hypernet2D as H
+    g = golden("ref_ops.npz")
+    mu = tuple(g[f"n{N}_mu"])
+    w, wp, x = g[f"n{N}_w"], g[f"n{N}_wp"], g[f"n{N}_x"]
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    Dxec, Dyec, JDxec, JDyec, Eye = H.get_ops(gx, gy)
+    r = H.inviscid_burgers_res2D_alt(w, gx, gy, 0.05, wp, mu, JDxec, JDyec)
+    assert rel(r, g[f"n{N}_res"]) <= 1e-15
+    r1 = H.inviscid_burgers_res2D(w, gx, gy, 0.05, wp, mu, Dxec, Dyec)
+    assert rel(r1, g[f"n{N}_res1d"]) <= 1e-15
+    J = H.inviscid_burgers_exact_jac2D(w, 0.05, JDxec, JDyec, Eye)
+    assert rel(J @ x, g[f"n{N}_jx"]) <= 1e-14
+    assert rel(J.solve(g[f"n{N}_res"]), g[f"n{N}_solve"]) <= 1e-13
+    # one implicit step by the reference's Newton with the drop-in callbacks
+    res = lambda v: H.inviscid_burgers_res2D_alt(v, gx, gy, 0.05, wp, mu)  # noqa: E731
+    jac = lambda v: H.inviscid_burgers_exact_jac2D(v, 0.05, grid_x=gx, grid_y=gy)  # noqa: E731
+    wn, norms = H.newton_raphson(res, jac, wp, 100, 1e-12)
+    assert norms[-1] / norms[0] < 1e-12 and len(norms) <= 8
+    ctx = make_ctx(N, mu)
+    snaps, _, _, _ = ctx.run(wp, 1)
+    assert rel(wn, snaps[:, 1]) <= 1e-13
+
+
+def test_plot_snaps_slices(gpu):
+    """plot_snaps (C/hypernet2D.py:3147-3180): the plotted lines are the
+    mid-row / mid-column slices of u the author pickled."""
+    import matplotlib
+    matplotlib.use("Agg")
+    from finitedifference_amd import hypernet2D as H
+    N, T = 64, 4
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    snaps = H.inviscid_burgers_implicit2D(gx, gy, np.ones(2 * N * N), 0.05, T, (5.19, 0.026),
+                                          verbose=0)
+    fig, ax1, ax2 = H.plot_snaps(gx, gy, snaps, [0, T], label="HDM")
+    U = snaps[:N * N].reshape(N, N, -1)
+    assert np.array_equal(ax1.lines[1].get_ydata(), U[N // 2, :, T])
+    assert np.array_equal(ax2.lines[1].get_ydata(), U[:, N // 2, T])
+    assert ax1.lines[0].get_label() == "HDM"
+    fig2, _, _ = H.plot_snaps(gx, gy, snaps, [2], fig_ax=(fig, ax1, ax2))
+    assert fig2 is fig and len(ax1.lines) == 3
+
+
+def test_snapshot_cache_snap_every_and_short_files(gpu, tmp_path):
+    """load_or_compute_snaps: a thinned (snap_every > 1) run is cached under a
+    name of its own, never under the reference's per-step name; a cached file
+    with too few columns is recomputed, not returned short."""
+    from finitedifference_amd import hypernet2D as H
+    N, T = 32, 12
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    w0 = np.ones(2 * N * N)
+    d = str(tmp_path / "ps")
+    thin = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d,
+                                   snap_every=4)
+    assert thin.shape[1] == 4
+    assert os.path.exists(os.path.join(d, "mu1_5.19+mu2_0.026+every4.npy"))
+    assert not os.path.exists(os.path.join(d, "mu1_5.19+mu2_0.026.npy"))
+    full = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d)
+    assert full.shape[1] == T + 1 and np.array_equal(full[:, ::4], thin)
+    np.save(os.path.join(d, "mu1_5.19+mu2_0.026.npy"), full[:, :5])  # a short cache
+    again = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d)
+    assert np.array_equal(again, full)
+
+
+def test_direct_npy_writer(gpu, tmp_path, monkeypatch):
+    """burg_run_npy (load_or_compute_snaps(direct=True)): the file the
+    library writes through its pinned double-buffered writer is np.save's
+    .npy of the reference's snapshot matrix, byte-identical to np.save of
+    burg_run's matrix; snap_every and multi-block files included."""
+    from finitedifference_amd import hypernet2D as H
+    N, T = 300, 9
+    gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
+    w0 = np.ones(2 * N * N)
+    ref = make_ctx(N).run(w0, T)[0]
+    np.save(tmp_path / "ref.npy", ref)
+    d = str(tmp_path / "ps")
+    got = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d, direct=True)
+    fn = os.path.join(d, "mu1_5.19+mu2_0.026.npy")
+    assert open(fn, "rb").read() == open(tmp_path / "ref.npy", "rb").read()
+    assert np.array_equal(got, ref)
+    monkeypatch.setenv("BURG_NPY_BLOCK_ROWS", "7001")  # 26 row blocks, ragged last one
+    ctx = make_ctx(N)
+    st = ctx.run_to_npy(w0, T, str(tmp_path / "thin.npy"), snap_every=4)
+    assert np.array_equal(np.load(tmp_path / "thin.npy"), ref[:, ::4])
+    assert st["loop_ms"] > 0 and st["flush_ms"] > 0
