@@ -88,7 +88,7 @@ def load(path=None):
     with _lock:
         if _lib is not None:
             return _lib
-        p = path or LIB_PATH
+        p = path or os.environ.get("BURG_LIB") or LIB_PATH  # BURG_LIB: A/B builds
         if not os.path.exists(p):
             raise RuntimeError(
                 f"{p} is missing: build the HIP extension first "

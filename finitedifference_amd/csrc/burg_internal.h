@@ -135,8 +135,6 @@ struct PipeArgs {
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid
-    int dbg;              // diagnostics (BURG_PIPE_DEBUG): bit 0 = check the wide state window
-    double *dbgbuf;       // diagnostics: 32 doubles (bit 2: tile 0, lane 0, diagonal 0 inputs)
     unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)
     unsigned *census;     // workgroups checked in (zeroed before every launch)
     StreamStats *stats;

@@ -499,12 +499,7 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
     a.err = c->d_err;
     a.census = c->d_err + 4;
-    if (const char *e = std::getenv("BURG_PIPE_DEBUG")) {  // diagnostics
-        a.dbg = std::atoi(e);
-        static double *dbgbuf = nullptr;
-        if ((a.dbg & 4) && !dbgbuf) (void)hipMalloc((void **)&dbgbuf, 32 * sizeof(double));
-        a.dbgbuf = dbgbuf;
-    }
+
     a.stats = c->d_sstats;
     if (c->ov_colc) a.colc = c->ov_colc;
     if (c->ov_lbc) a.cf.lbc = c->ov_lbc;
@@ -525,18 +520,6 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
     float t = 0.f;
     HIPCHK(hipEventElapsedTime(&t, c->ev0, c->ev1));
     *ms += t;
-    if (pipe) {
-        const PipeArgs pa = pipe_args(c, L, origin, K);
-        if ((pa.dbg & 4) && pa.dbgbuf) {
-            double v[24];
-            (void)hipMemcpy(v, pa.dbgbuf, sizeof v, hipMemcpyDeviceToHost);
-            std::fprintf(stderr, "[pipe dbg] loader: win[0][0][0] %g %g ring %g %g e %g L %g "
-                         "origin %g nf %g\n", v[16], v[17], v[18], v[19], v[20], v[21], v[22], v[23]);
-            std::fprintf(stderr, "[pipe dbg] pu %g pv %g hx %g src %g sl %g ay %g lb %g e %g %g n %g %g "
-                         "o %g %g bu %g bv %g ok %g\n", v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7],
-                         v[8], v[9], v[10], v[11], v[12], v[13], v[14], v[15]);
-        }
-    }
     unsigned err[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
     if (err[0]) {

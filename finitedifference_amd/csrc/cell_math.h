@@ -131,12 +131,14 @@ struct MarchCell {
         if constexpr (FAST) {
             // operands +0 or of magnitude in [2^-900, 2^900]: div2_normal's exact
             // range (-0 would come out +0; NaN fails too: the streaming engines
-            // rely on it); q in sqrt_normal's exact range (a negative
-            // discriminant goes to the IEEE path, which reports the NaN)
+            // rely on it).  q > 0: q = 0.25 + mm is either <= 0 or >= 2^-55
+            // (Sterbenz), and sqrt_normal is exact there; a zero or negative
+            // discriminant goes to the IEEE path, which reports a NaN.
+            // Bitwise & / |: no short-circuit branches on the critical path.
             const double au = fabs(cu), av = fabs(cv);
-            range_ok = ((au >= 0x1p-900 && au <= 0x1p+900) || __double_as_longlong(cu) == 0) &&
-                       ((av >= 0x1p-900 && av <= 0x1p+900) || __double_as_longlong(cv) == 0) &&
-                       (q >= 0x1p-900 && q <= 0x1p+900);
+            range_ok = (((au >= 0x1p-900) & (au <= 0x1p+900)) | (__double_as_longlong(cu) == 0)) &
+                       (((av >= 0x1p-900) & (av <= 0x1p+900)) | (__double_as_longlong(cv) == 0)) &
+                       (q > 0.0);
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

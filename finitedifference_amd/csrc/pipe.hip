@@ -85,9 +85,21 @@ template <int W>
 constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
 constexpr int kNI = 64;   // south inbox ring (diagonals), power of two
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
-constexpr int kLA = 16;   // poll window (diagonals ahead of a compute wave's progress)
-constexpr int kWin = 16;  // wide tiles: LDS window of previous states per compute wave (diagonals)
-constexpr int kUw = 8;    // wide tiles: diagonals per block (progress / store completion published)
+#ifndef BURG_KLA
+#define BURG_KLA 16
+#endif
+#ifndef BURG_NARROW_U
+#define BURG_NARROW_U 4
+#endif
+constexpr int kLA = BURG_KLA;  // poll window (diagonals ahead of a compute wave's progress)
+#ifndef BURG_KWIN
+#define BURG_KWIN 16
+#endif
+#ifndef BURG_UW
+#define BURG_UW 8
+#endif
+constexpr int kWin = BURG_KWIN;  // wide tiles: LDS window of previous states per compute wave (diagonals)
+constexpr int kUw = BURG_UW;     // wide tiles: diagonals per block (progress / store completion published)
 
 __device__ __forceinline__ d2 as_d2(v4u v)
 {
@@ -184,6 +196,10 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void *p, size_t byt
 
 __device__ __forceinline__ long long now_rt() { return (long long)__builtin_amdgcn_s_memrealtime(); }
 
+// any lane: the ballot mask compared on the scalar unit (hipcc's __any goes
+// through a VGPR select and a vector compare)
+__device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
+
 
 // LDS accesses that must not be cached in registers or merged (polled / handed
 // off between waves).  Explicit address space 3: a volatile access through a
@@ -222,6 +238,7 @@ struct PipeLds {
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
+    v4u dump[WIDE ? 4 : 1][WIDE ? kWave : 1];  // wide: write target of lanes with nothing to hand off
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
@@ -240,7 +257,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
-    constexpr int U = WIDE ? kUw : 4;  // diagonals per block (progress published per block)
+    constexpr int U = WIDE ? kUw : BURG_NARROW_U;  // diagonals per block (progress published per block)
     __shared__ PipeLds<W, SWEEP> sm;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -485,21 +502,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                         rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * L * kWave, (size_t)L * kWave * 16);
                     long long e = (a.origin + nf[k] - W) % L;
                     e = e < 0 ? e + L : e;
-                    if (a.dbg & 2) {
-                        // diagnostics: register staging instead of LDS-DMA
-                        for (; nf[k] < lim; ++nf[k]) {
-                            const v4u x = __builtin_amdgcn_raw_buffer_load_b128(
-                                ring, (unsigned)e * 1024u + lane * 16u, 0, 16);
-                            lds_st(&sm.win[k][nf[k] & (kWin - 1)][lane], x);
-                            e = e + 1 == L ? 0 : e + 1;
-                        }
-                    } else {
-                        for (; nf[k] < lim; ++nf[k]) {
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                                ring, (__attribute__((address_space(3))) void *)&sm.win[k][nf[k] & (kWin - 1)][0],
-                                16, (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
-                            e = e + 1 == L ? 0 : e + 1;
-                        }
+                    for (; nf[k] < lim; ++nf[k]) {
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                            ring, (__attribute__((address_space(3))) void *)&sm.win[k][nf[k] & (kWin - 1)][0],
+                            16, (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
+                        e = e + 1 == L ? 0 : e + 1;
                     }
                     issued = true;
                 }
@@ -507,15 +514,6 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             }
             if (issued) {
                 __builtin_amdgcn_s_waitcnt(0);  // the DMA rows have landed in LDS
-                if ((a.dbg & 4) && a.dbgbuf && wg == 0 && lane == 0 && lds_ldi(&sm.filled[0]) == 0) {
-                    const d2 w0v = as_d2(lds_ld(&sm.win[0][0][0]));
-                    long long e0 = (a.origin - W) % L;
-                    e0 = e0 < 0 ? e0 + L : e0;
-                    const d2 g0 = a.ring[(size_t)e0 * kWave];
-                    const double v[8] = {w0v.x, w0v.y, g0.x, g0.y, (double)e0, (double)L,
-                                         (double)a.origin, (double)nf[0]};
-                    for (int i = 0; i < 8; ++i) a.dbgbuf[16 + i] = v[i];
-                }
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                     if (k < nval && lane == 0) lds_sti(&sm.filled[k], nf[k]);
@@ -569,8 +567,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
                                              (size_t)a.L * kWave * 16);
     const __amdgpu_buffer_rsrc_t wbox = rsrc(a.wbox, a.wbox_bytes);
-    const __amdgpu_buffer_rsrc_t sbox = rsrc(a.sbox, a.sbox_bytes);
-    const __amdgpu_buffer_rsrc_t hout = rsrc(a.halo_out, a.halo_out ? a.halo_bytes : 0);
+    // north outflow target: the north tile's south box, or the halo ring
+    const __amdgpu_buffer_rsrc_t nrs = north_host ? rsrc(a.halo_out, a.halo_bytes)
+                                                  : rsrc(a.sbox, a.sbox_bytes);
     const unsigned lane16 = lane * 16u;
     // outbound bases (slot offsets added per step)
     const unsigned eb = ((unsigned)(tile + 1) * kR * kWave + lane) * G;  // east tile's west box
@@ -582,8 +581,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     v4u(*src_w)[kWave] = k == 0 ? sm.inw : sm.ewe[k - 1];
     v4u *const my_st = &sm.st[k][0][0];
     v4u *const my_st0 = &sm.st0[k][0][0];
-    const long long L = a.L;
-    long long pw = a.origin;
+    const unsigned Lu = (unsigned)a.L;  // < 2^21 entries (one descriptor)
+    unsigned pw = (unsigned)a.origin;
     const v4u lempty = lds_empty_g();
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
@@ -665,22 +664,23 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         MarchCell::Pre p = pre_of(in);
         const MarchCell::Row rw{ay, hy, lbu};
         // ---- wait until inputs are deposited and outbound slots are granted
+        // (bitwise & / |: no short-circuit branches)
         auto blocked = [&](const In &v) -> bool {
-            bool b = (need_w && !l_is_data(v.gw)) || (lane == 0 && need_s && !l_is_data(v.gs));
-            b |= east_lds && out_e && v.ee != kLdsEmptyHi;
-            b |= east_glob && out_e && q >= v.pe;
-            b |= out_n && t >= v.pn;
+            bool b = (need_w & !l_is_data(v.gw)) | ((lane == 0) & need_s & !l_is_data(v.gs));
+            b |= east_lds & out_e & (v.ee != kLdsEmptyHi);
+            b |= east_glob & out_e & (q >= v.pe);
+            b |= out_n & (t >= v.pn);
             if constexpr (WIDE) b |= s >= v.pf;
             return b;
         };
-        if (__builtin_expect(__any(blocked(in)), 0)) {
+        if (__builtin_expect(any_lane(blocked(in)), 0)) {
             const long long t0 = now_rt();
             ++slow_n;
             for (;;) {
                 ++spins;
                 __builtin_amdgcn_s_sleep(1);
                 in = fetch(s);
-                if (!__any(blocked(in))) break;
+                if (!any_lane(blocked(in))) break;
                 if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                     // which input / grant was missing (diagnosis in err[3] >> 8)
                     unsigned why = 0;
@@ -704,21 +704,6 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // wide tiles: the previous state arrives with the window fill
             if constexpr (WIDE) p = pre_of(in);
         }
-        if (WIDE && (a.dbg & 1)) {
-            // diagnostics: the window row must equal the ring entry it copies
-            long long e = (a.origin + s - W) % L;
-            e = e < 0 ? e + L : e;
-            const v4u r0 = ld_plain(ring, (unsigned)e * 1024u + lane16);
-            const bool bad = valid && rowok && (r0.x != in.xs.x || r0.y != in.xs.y ||
-                                                r0.z != in.xs.z || r0.w != in.xs.w);
-            // lanes whose window row differs from the ring: [0] initial state, [1] later steps
-            const unsigned long long b0 = __ballot(bad && t < W), b1 = __ballot(bad && t >= W);
-            if (lane == 0) {
-                if (b0) atomicAdd(&a.stats->why[0], (unsigned long long)__popcll(b0));
-                if (b1) atomicAdd(&a.stats->why[1], (unsigned long long)__popcll(b1));
-                if (b0 | b1) atomicAdd(&a.stats->why[2], 1ull);
-            }
-        }
         // ---- the cell's chain
         if (at0) {
             const d2 gv = as_d2(in.gw);
@@ -731,13 +716,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         double oe0, oe1, on0, on1, o0, o1;
         bool ok;
         MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
-        if ((a.dbg & 4) && tile == 0 && lane == 0 && s == 0 && a.dbgbuf) {
-            const d2 xx = as_d2(in.xs);
-            const double v[16] = {xx.x, xx.y, p.hx, as_d2(in.cs).y, 0.0, ay, lbu, e0, e1, n0, n1,
-                                  o0, o1, p.bu, p.bv, (double)ok};
-            for (int i = 0; i < 16; ++i) a.dbgbuf[i] = v[i];
-        }
-        if (__builtin_expect(__any(!ok && valid && rowok), 0)) {
+        if (__builtin_expect(any_lane(!ok & valid & rowok), 0)) {
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             ++ieee_n;
             // the only place a non-finite state can appear (the fast path's
@@ -757,27 +736,42 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // wide tiles: the loader wave reads this entry back (sc1 DMA) W
         // diagonals later, so it is stored write-through to L2 (sc1): the
         // store's vmcnt then completes at L2, which the done[] protocol needs
-        if constexpr (WIDE) st_dev(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
-        else st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
-        pw = pw + 1 == L ? 0 : pw + 1;
+        if constexpr (WIDE) st_dev(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+        else st_plain(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+        pw = pw + 1 == Lu ? 0u : pw + 1;
         const v4u eo = as_v4u(oe0, oe1);
         const int aq = a.qbase + q;
-        if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
+        // (LDS writes go to a selected address -- a dump slot for lanes
+        // that have nothing to write -- instead of an exec-masked branch)
+        if constexpr (WIDE) {
+            if (east_lds) lds_st(out_e ? (void *)&sm.ewe[k][q & (kRL - 1)][lane] : (void *)&sm.dump[k][lane], eo);
+        } else {
+            if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
+        }
         // wide tiles issue every store on every diagonal (out-of-range offsets
         // are dropped), so the compiler's vmcnt for the prefetch is exact
         if (WIDE || east_glob)
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
         if (WIDE || has_north) {
+            // one store flavour for both targets: sc0 sc1 (system scope) reaches
+            // the host / peer halo ring and is write-through like sc1 for the
+            // device mailboxes (consumers poll with sc1 / sc0 sc1 loads)
             const v4u no = as_v4u(on0, on1);
-            const unsigned off = out_n && c < ncol_real
+            const unsigned off = (out_n & (c < ncol_real))
                                      ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
                                      : kOOB;
-            if (north_host) st_sys(hout, off, no);
-            else st_dev(sbox, off, no);
+            st_sys(nrs, off, no);
         }
         // consumed inbound slots back to empty
-        if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
-        if (need_s && lane == 0) lds_st(&sm.ins[k][s & (kNI - 1)], lempty);
+        if constexpr (WIDE) {
+            if (has_west) lds_st(need_w ? (void *)&src_w[q & (kRL - 1)][lane] : (void *)&sm.dump[k][lane], lempty);
+            if (has_south)
+                lds_st((need_s & (lane == 0)) ? (void *)&sm.ins[k][s & (kNI - 1)] : (void *)&sm.dump[k][lane],
+                       lempty);
+        } else {
+            if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
+            if (need_s && lane == 0) lds_st(&sm.ins[k][s & (kNI - 1)], lempty);
+        }
         if constexpr (SWEEP) {
             // the lane finished the first step of its next trajectory: switch
             if (in.nt && atE) {
@@ -805,8 +799,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // every store older than this block's predecessor has completed
             // (at most 3 stores per diagonal, no loads): the loader may read
             // ring entries written before diagonal sb - U
-            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-            static_assert(3 * kUw == 24, "vmcnt covers one block of stores");
+            if constexpr (kUw == 8) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            static_assert(kUw == 8 || kUw == 4, "vmcnt covers one block of stores");
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
         if (lane == 0) lds_sti(&sm.prog[k], sb);
