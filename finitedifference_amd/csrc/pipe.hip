@@ -232,7 +232,7 @@ struct PipeLds {
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
-    double lbt[kSW][kWave];                        // sweep: inlet term of trajectory j, by row
+    double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
     v4u cc[4][W];           // per wave: {hx, src} of the tile's columns
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
@@ -242,6 +242,7 @@ struct PipeLds {
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
+    int pe_row[kWave];      // east grant of wave 3, per row: steps whose slot is free
     int done[4];            // wide: per compute wave, diagonals whose stores completed
     int filled[4];          // wide: per compute wave, window filled below this diagonal
 };
@@ -253,6 +254,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     static_assert(!is_wide<W>() || sizeof(PipeLds<W, SWEEP>::win) <= 65536,
                   "LDS-DMA window must sit below 64 KB");
     constexpr bool WIDE = is_wide<W>();
+    // three narrow W=8 workgroups per CU: room for 8 slab processes sharing one
+    // GPU (the 750^2 C5 case, tests/test_gpu_parity.py) with all grids resident
+    static_assert(W != 8 || SWEEP || 3 * sizeof(PipeLds<W, SWEEP>) <= 160 * 1024,
+                  "narrow W=8 LDS image must fit three times in a CU");
     static_assert(W == 8 || W == 16 || (WIDE && W <= 1024 && (W & (W - 1)) == 0),
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
@@ -313,6 +318,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     for (int i = threadIdx.x; i < kRL * kWave; i += kThreads) (&sm.inw[0][0])[i] = lds_empty_g();
     for (int i = threadIdx.x; i < 4 * kNI; i += kThreads) (&sm.ins[0][0])[i] = lds_empty_g();
     if (threadIdx.x < 6) sm.perm[threadIdx.x] = 0;
+    if (threadIdx.x < kWave) sm.pe_row[threadIdx.x] = 0;
     if (threadIdx.x < 4) {
         sm.prog[threadIdx.x] = 0;
         sm.done[threadIdx.x] = 0;
@@ -396,9 +402,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const bool wS = rS && qs <= pS + kLA;
             const bool wN = rN && qn + top <= pS + 2 * kLA;
             const bool wW = rW && qw * W + lane <= p0 + kLA;
-            // (the east grant is a minimum over all rows: every row's slot of
-            // step qe is polled once row 0 approaches it)
-            const bool wE = rE && qe * W + (W - 1) <= p3 + 2 * kLA;
+            const bool wE = rE && qe * W + (W - 1) + lane <= p3 + 2 * kLA;
             const int aS = a.qbase + (qs >> LW), aN = a.qbase + (qn >> LW);
             const int aW = a.qbase + qw, aE = a.qbase + qe;
             const int cS = qs & (W - 1), cN = qn & (W - 1);
@@ -448,13 +452,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 prog = true;
             }
             // grants: north of wave k = the first diagonal not yet verified
-            // free over its 16 stream lanes; east of wave 3 = min over rows
+            // free over its 16 stream lanes; east of wave 3 = per row (a
+            // minimum over rows would tie row 0's progress to row 63's)
             int vN = actN ? qn : INT_MAX;
             for (int m = 1; m < kSL; m <<= 1) vN = min(vN, __shfl_xor(vN, m));
-            int vE = actE ? qe : INT_MAX;
-            for (int m = 1; m < kWave; m <<= 1) vE = min(vE, __shfl_xor(vE, m));
             if (jS == 0 && kval) lds_sti(&sm.perm[kq], vN);
-            if (lane == 0) lds_sti(&sm.perm[4], vE);
+            if (actE) lds_sti(&sm.pe_row[lane], qe);
             const long long tn = now_rt();
             if (__any(prog) || !__any(wS || wN || wW || wE)) {
                 t_prog = tn;  // progress, or nothing due (the compute waves time out themselves)
@@ -557,8 +560,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // inlet term of the lane's trajectory (sweep: lb of trajectory jl, lb_next
     // of jl + 1; qn = first step of trajectory jl + 1, whose W columns read
     // the initial state -- every trajectory starts from w0)
-    double lb = SWEEP ? sm.lbt[0][lane] : a.cf.lbc[r];
-    double lb_next = SWEEP ? sm.lbt[min(1, nsw - 1)][lane] : lb;
+    double lb = SWEEP ? sm.lbt[0][SWEEP ? lane : 0] : a.cf.lbc[r];
+    double lb_next = SWEEP ? sm.lbt[min(1, nsw - 1)][SWEEP ? lane : 0] : lb;
     int qn = SWEEP ? a.T : INT_MAX, jl = 0;
     // LDS rows of the src table for trajectories jl and jl + 1 (clamped)
     typedef __attribute__((address_space(3))) const double lds_f64;
@@ -590,11 +593,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     bool aborted = false;
 
 
-    // LDS inputs of diagonal s, read at the end of diagonal s - 1
+    // LDS inputs of diagonal s (read at the end of diagonal s - 1, or after
+    // the block's readiness check for the first diagonal of a block)
     struct In {
         v4u xs, cs, gw, gs;
-        int pn, pe, pf;
-        unsigned ee;
         bool nt;     // sweep: first step of the lane's next trajectory (state reset)
         double src;  // sweep: the column's source term of the step's trajectory
     };
@@ -603,7 +605,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const int c = t & (W - 1);
         const int q = t >> LW;
         const bool valid = (unsigned)t < (unsigned)KW;
-        const bool need_w = has_west && c == 0 && valid && rowok;
+        const bool need_w = has_west & (c == 0) & valid & rowok;
         In in;
         if constexpr (SWEEP) {
             in.nt = q >= qn;
@@ -614,96 +616,91 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.xs = my_st[(s & (W - 1)) * kWave + lane];
             in.src = 0.0;
         } else {
-            // wide: the window's fill mark first, then the slot (LDS reads of
-            // one wave complete in order)
             in.nt = false;
             in.src = 0.0;
-            in.pf = lds_ldi(&sm.filled[k]);
             in.xs = lds_ld(&sm.win[k][s & (kWin - 1)][lane]);
         }
         in.cs = sm.cc[k][c];
         in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
-        in.gs = lds_ld(has_south && s < KW ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
-        in.pn = lds_ldi(&sm.perm[k]);
-        in.pe = lds_ldi(&sm.perm[4]);
-        in.ee = east_lds ? lds_ld32((const char *)&sm.ewe[k][q & (kRL - 1)][lane] + 4) : kLdsEmptyHi;
+        in.gs = lds_ld((has_south & (s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
         return in;
     };
 
-    // one diagonal; returns false when the launch is aborted
-    auto diagonal = [&](const int s, In &in) -> bool {
+    // Readiness of a whole block of diagonals [sb, sb + U): every inflow it
+    // consumes is deposited, every outbound slot it fills is granted and (wide
+    // tiles) every previous state is in the window.  Checked once per block,
+    // so the diagonals themselves run without waits.  Returns the missing
+    // kinds (0: ready; bits as err[3] >> 8), wave-uniform.
+    auto block_missing = [&](int sb) -> unsigned {
+        unsigned why = 0;
+        const int t0 = sb - lane;  // the lane's local time at the block's first diagonal
+        const int c0 = t0 & (W - 1);
+        if (has_west) {  // the lane's column-0 diagonal in the block (U <= W: at most one)
+            const int uw = (W - c0) & (W - 1);
+            const int tw = t0 + uw;
+            const bool nw = (uw < U) & ((unsigned)tw < (unsigned)KW) & rowok;
+            const v4u g = lds_ld(&src_w[(tw >> LW) & (kRL - 1)][lane]);
+            if (any_lane(nw & !l_is_data(g))) why |= 1u;
+        }
+        if (has_south) {  // lane i checks the inflow of diagonal sb + i
+            const int d = sb + lane;
+            const unsigned hi = lds_ld32((const char *)&sm.ins[k][d & (kNI - 1)] + 4);
+            if (any_lane((lane < U) & (d < KW) & (hi == kLdsEmptyHi))) why |= 2u;
+        }
+        const int ue = (W - 1 - c0) & (W - 1);  // the lane's column W-1 diagonal in the block
+        const int te = t0 + ue;
+        const bool oe = (ue < U) & ((unsigned)te < (unsigned)KW) & rowok;
+        if (east_lds) {
+            const unsigned hi = lds_ld32((const char *)&sm.ewe[k][(te >> LW) & (kRL - 1)][lane] + 4);
+            if (any_lane(oe & (hi != kLdsEmptyHi))) why |= 4u;
+        }
+        if (east_glob) {
+            const int pe = lds_ldi(&sm.pe_row[lane]);
+            if (any_lane(oe & ((te >> LW) >= pe))) why |= 8u;
+        }
+        if (has_north) {  // the top lane's last local time in the block
+            const int pn = lds_ldi(&sm.perm[k]);
+            const int th = min(sb - top + U - 1, KW - 1);
+            if (any_lane((th >= 0) & (th >= pn))) why |= 16u;
+        }
+        if constexpr (WIDE) {
+            if (any_lane(lds_ldi(&sm.filled[k]) < sb + U)) why |= 32u;
+        }
+        return why;
+    };
+
+    // one diagonal (no waits: its block was checked); `next` = also read the
+    // inputs of diagonal s + 1 (inside the block)
+    auto diagonal = [&](const int s, const bool next, In &in) {
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
         const bool valid = (unsigned)t < (unsigned)KW;
         const bool at0 = c == 0, atE = c == W - 1;
-        const bool need_w = has_west && at0 && valid && rowok;
-        const bool need_s = has_south && s < KW;  // wave-uniform (lane 0 consumes)
-        const bool out_e = atE && valid && rowok;
-        const bool out_n = lane == top && valid && has_north;
+        const bool need_w = has_west & at0 & valid & rowok;
+        const bool need_s = has_south & (s < KW);  // wave-uniform (lane 0 consumes)
+        const bool out_e = atE & valid & rowok;
+        const bool out_n = (lane == top) & valid & has_north;
         // ---- inflow-independent part of the cell (MarchCell::pre, same op order)
         const double lbu = SWEEP && in.nt ? lb_next : lb;
-        auto pre_of = [&](const In &v) -> MarchCell::Pre {
-            const d2 x = as_d2(v.xs);
-            const d2 co = as_d2(v.cs);
+        MarchCell::Pre p;
+        {
+            const d2 x = as_d2(in.xs);
+            const d2 co = as_d2(in.cs);
             const double pu = x.x, pv = x.y;
             const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
-            const double srcc = SWEEP ? v.src : co.y;
+            const double srcc = SWEEP ? in.src : co.y;
             const double sl = (col0_tile && at0) ? srcc + lbu : srcc;
-            MarchCell::Pre q;
-            q.hx = hx;
+            p.hx = hx;
             const double hu = 0.5 * pu;
-            q.xfp = ax * (hu * pu);
-            q.xhp = ax * (hu * pv);
-            q.yhp = ay * (hu * pv);
-            q.ygp = ay * ((0.5 * pv) * pv);
-            q.bu = ((pu - q.xfp) - q.yhp) + sl;
-            q.bv = (pv - q.ygp) - q.xhp;
-            return q;
-        };
-        MarchCell::Pre p = pre_of(in);
-        const MarchCell::Row rw{ay, hy, lbu};
-        // ---- wait until inputs are deposited and outbound slots are granted
-        // (bitwise & / |: no short-circuit branches)
-        auto blocked = [&](const In &v) -> bool {
-            bool b = (need_w & !l_is_data(v.gw)) | ((lane == 0) & need_s & !l_is_data(v.gs));
-            b |= east_lds & out_e & (v.ee != kLdsEmptyHi);
-            b |= east_glob & out_e & (q >= v.pe);
-            b |= out_n & (t >= v.pn);
-            if constexpr (WIDE) b |= s >= v.pf;
-            return b;
-        };
-        if (__builtin_expect(any_lane(blocked(in)), 0)) {
-            const long long t0 = now_rt();
-            ++slow_n;
-            for (;;) {
-                ++spins;
-                __builtin_amdgcn_s_sleep(1);
-                in = fetch(s);
-                if (!any_lane(blocked(in))) break;
-                if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
-                    // which input / grant was missing (diagnosis in err[3] >> 8)
-                    unsigned why = 0;
-                    why |= __any(need_w && !l_is_data(in.gw)) ? 1u : 0u;
-                    why |= __any(lane == 0 && need_s && !l_is_data(in.gs)) ? 2u : 0u;
-                    why |= __any(east_lds && out_e && in.ee != kLdsEmptyHi) ? 4u : 0u;
-                    why |= __any(east_glob && out_e && q >= in.pe) ? 8u : 0u;
-                    why |= __any(out_n && t >= in.pn) ? 16u : 0u;
-                    if (WIDE && s >= in.pf) why |= 32u;
-                    if (lane == 0 && !lds_ldi(&sm.perm[5])) {
-                        lds_sti(&sm.perm[5], 1);
-                        if (atomicOr(a.err, 1u) == 0) {
-                            a.err[1] = (unsigned)tile;
-                            a.err[2] = (unsigned)s;
-                            a.err[3] = 32u | (why << 8);
-                        }
-                    }
-                    return false;
-                }
-            }
-            // wide tiles: the previous state arrives with the window fill
-            if constexpr (WIDE) p = pre_of(in);
+            p.xfp = ax * (hu * pu);
+            p.xhp = ax * (hu * pv);
+            p.yhp = ay * (hu * pv);
+            p.ygp = ay * ((0.5 * pv) * pv);
+            p.bu = ((pu - p.xfp) - p.yhp) + sl;
+            p.bv = (pv - p.ygp) - p.xhp;
         }
+        const MarchCell::Row rw{ay, hy, lbu};
         // ---- the cell's chain
         if (at0) {
             const d2 gv = as_d2(in.gw);
@@ -749,7 +746,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
         }
         // wide tiles issue every store on every diagonal (out-of-range offsets
-        // are dropped), so the compiler's vmcnt for the prefetch is exact
+        // are dropped): exactly 3 per diagonal, which the vmcnt of done[] counts
         if (WIDE || east_glob)
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
         if (WIDE || has_north) {
@@ -780,24 +777,23 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 lb = lb_next;
                 src_cur = src_nxt;
                 const int jn = min(jl + 1, nsw - 1);
-                lb_next = sm.lbt[jn][lane];
+                lb_next = sm.lbt[jn][SWEEP ? lane : 0];
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
-        in = fetch(s + 1);
-        return true;
+        if (next) in = fetch(s + 1);
     };
 
     const int total = KW + kWave - 1;
-    In in = fetch(0);
     // Land the prologue's global loads (row coefficients) here: a first use
     // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
     // in flight -- into every diagonal.
     __builtin_amdgcn_s_waitcnt(0);
-    for (int sb = 0; sb < total && !aborted; sb += U) {
+    In in;
+    for (int sb = 0; sb < total; sb += U) {
         if constexpr (WIDE) {
             // every store older than this block's predecessor has completed
-            // (at most 3 stores per diagonal, no loads): the loader may read
+            // (exactly 3 stores per diagonal, no loads): the loader may read
             // ring entries written before diagonal sb - U
             if constexpr (kUw == 8) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
             else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -805,10 +801,33 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
         if (lane == 0) lds_sti(&sm.prog[k], sb);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!aborted && !diagonal(sb + u, in)) aborted = true;
+        unsigned why = block_missing(sb);
+        if (__builtin_expect(why != 0, 0)) {
+            const long long t0 = now_rt();
+            ++slow_n;
+            for (;;) {
+                ++spins;
+                __builtin_amdgcn_s_sleep(1);
+                why = block_missing(sb);
+                if (!why) break;
+                if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
+                    if (lane == 0 && !lds_ldi(&sm.perm[5])) {
+                        lds_sti(&sm.perm[5], 1);
+                        if (atomicOr(a.err, 1u) == 0) {
+                            a.err[1] = (unsigned)tile;
+                            a.err[2] = (unsigned)sb;
+                            a.err[3] = 32u | (why << 8);
+                        }
+                    }
+                    aborted = true;
+                    break;
+                }
+            }
+            if (aborted) break;
         }
+        in = fetch(sb);
+#pragma unroll
+        for (int u = 0; u < U; ++u) diagonal(sb + u, u + 1 < U, in);
     }
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, spins);
