@@ -238,7 +238,7 @@ struct PipeLds {
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
-    v4u dump[WIDE ? 4 : 1][WIDE ? kWave : 1];  // wide: write target of lanes with nothing to hand off
+    v4u dump[WIDE ? kWave : 1];  // wide: write target of lanes with nothing to hand off (shared)
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
@@ -246,6 +246,12 @@ struct PipeLds {
     int done[4];            // wide: per compute wave, diagonals whose stores completed
     int filled[4];          // wide: per compute wave, window filled below this diagonal
 };
+
+// The LDS image is DYNAMIC shared memory (launch_pipe passes its size): with a
+// static image the compiler pads the kernel's VGPR allocation up to what the
+// LDS-limited occupancy would leave (176 registers for a 90 KB image), and two
+// 6-wave workgroups then no longer fit one CU.
+extern __shared__ __attribute__((aligned(16))) unsigned char pipe_lds_image[];
 
 template <int W, bool SWEEP>
 __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
@@ -263,7 +269,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
     constexpr int U = WIDE ? kUw : BURG_NARROW_U;  // diagonals per block (progress published per block)
-    __shared__ PipeLds<W, SWEEP> sm;
+    PipeLds<W, SWEEP> &sm = *reinterpret_cast<PipeLds<W, SWEEP> *>(pipe_lds_image);
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
@@ -741,7 +747,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
         if constexpr (WIDE) {
-            if (east_lds) lds_st(out_e ? (void *)&sm.ewe[k][q & (kRL - 1)][lane] : (void *)&sm.dump[k][lane], eo);
+            if (east_lds) lds_st(out_e ? (void *)&sm.ewe[k][q & (kRL - 1)][lane] : (void *)&sm.dump[lane], eo);
         } else {
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
         }
@@ -761,9 +767,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         // consumed inbound slots back to empty
         if constexpr (WIDE) {
-            if (has_west) lds_st(need_w ? (void *)&src_w[q & (kRL - 1)][lane] : (void *)&sm.dump[k][lane], lempty);
+            if (has_west) lds_st(need_w ? (void *)&src_w[q & (kRL - 1)][lane] : (void *)&sm.dump[lane], lempty);
             if (has_south)
-                lds_st((need_s & (lane == 0)) ? (void *)&sm.ins[k][s & (kNI - 1)] : (void *)&sm.dump[k][lane],
+                lds_st((need_s & (lane == 0)) ? (void *)&sm.ins[k][s & (kNI - 1)] : (void *)&sm.dump[lane],
                        lempty);
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
@@ -795,8 +801,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // every store older than this block's predecessor has completed
             // (exactly 3 stores per diagonal, no loads): the loader may read
             // ring entries written before diagonal sb - U
-            if constexpr (kUw == 8) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+            // s_waitcnt vmcnt(24) / vmcnt(12) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]
+            // | lgkmcnt[11:8] | vmcnt[5:4] << 14; expcnt / lgkmcnt at their max =
+            // no wait).  A builtin, not inline asm: asm would keep the compiler
+            // from proving the kernel AGPR-free, and the unused AGPR budget it
+            // then reserves caps the waves per SIMD.
+            if constexpr (kUw == 8) __builtin_amdgcn_s_waitcnt((1 << 14) | (0xF << 8) | (7 << 4) | 8);
+            else __builtin_amdgcn_s_waitcnt((0xF << 8) | (7 << 4) | 12);
             static_assert(kUw == 8 || kUw == 4, "vmcnt covers one block of stores");
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
@@ -868,17 +879,37 @@ const void *kernel_of(int W)
 
 const void *pipe_fn(int W, bool sweep) { return sweep ? kernel_of<true>(W) : kernel_of<false>(W); }
 
-// dynamic LDS that pins the wide-tile engine to `per_cu` workgroups per CU
-// (its static image is small enough for several); narrow tiles keep theirs
-size_t pipe_dyn_lds(int W, const void *fn, int per_cu)
+template <bool SWEEP>
+size_t image_of(int W)
 {
-    if (W <= 16) return 0;
-    hipFuncAttributes at{};
-    if (hipFuncGetAttributes(&at, fn) != hipSuccess) return 0;
+    switch (W) {
+    case 8: return sizeof(PipeLds<8, SWEEP>);
+    case 16: return sizeof(PipeLds<16, SWEEP>);
+    case 32: return sizeof(PipeLds<32, SWEEP>);
+    case 64: return sizeof(PipeLds<64, SWEEP>);
+    case 128: return sizeof(PipeLds<128, SWEEP>);
+    case 256: return sizeof(PipeLds<256, SWEEP>);
+    case 512: return sizeof(PipeLds<512, SWEEP>);
+    case 1024: return sizeof(PipeLds<1024, SWEEP>);
+    default: return 0;
+    }
+}
+
+// LDS bytes per workgroup: the image, padded for the wide-tile engine so that
+// exactly `per_cu` workgroups share a CU (narrow tiles keep their image size)
+size_t pipe_dyn_lds(int W, bool sweep, int per_cu)
+{
+    const size_t img = sweep ? image_of<true>(W) : image_of<false>(W);
+    if (W <= 16) return img;
     const size_t lds_cu = 160 * 1024;
     const size_t want = lds_cu / (size_t)(per_cu + 1) + 1024;
-    if (want > lds_cu / (size_t)per_cu) return 0;
-    return at.sharedSizeBytes >= want ? 0 : want - at.sharedSizeBytes;
+    if (want > lds_cu / (size_t)per_cu) return img;
+    return img >= want ? img : want;
+}
+
+bool set_lds_limit(const void *fn, size_t bytes)
+{
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
 }
 
 int pipe_per_cu_opt()
@@ -909,7 +940,8 @@ int pipe_max_resident_blocks(int W, bool sweep)
         return -3;
     const void *fn = pipe_fn(W, sweep);
     if (!fn) return -1;
-    const size_t dyn = pipe_dyn_lds(W, fn, pipe_per_cu_opt());
+    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt());
+    if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
         hipSuccess)
         return -3;
@@ -923,7 +955,8 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
     const void *fn = pipe_fn(W, sweep);
     if (!fn) return -1;
-    const size_t dyn = pipe_dyn_lds(W, fn, pipe_per_cu_opt());
+    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt());
+    if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return -1;
     // the census counter starts at zero in every launch
     if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;
     PipeArgs args = a;
