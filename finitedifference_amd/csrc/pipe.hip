@@ -63,6 +63,7 @@
 // (s_memrealtime): a wave that gives up sets the error word and the LDS abort
 // flag, and the launch drains.
 #include <climits>
+#include <type_traits>
 
 #include "burg_internal.h"
 #include "cell_math.h"
@@ -205,14 +206,18 @@ __device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballo
 // off between waves).  Explicit address space 3: a volatile access through a
 // generic pointer becomes a flat_load, which waits on vmcnt (and so on every
 // older global store of the wave) -- the coupling this engine exists to avoid.
-typedef __attribute__((address_space(3))) v4u lds_v4u;
-typedef __attribute__((address_space(3))) unsigned lds_u32;
-typedef __attribute__((address_space(3))) int lds_i32;
-__device__ __forceinline__ v4u lds_ld(const void *p) { return *(volatile lds_v4u *)p; }
-__device__ __forceinline__ void lds_st(void *p, v4u v) { *(volatile lds_v4u *)p = v; }
-__device__ __forceinline__ unsigned lds_ld32(const void *p) { return *(volatile lds_u32 *)p; }
-__device__ __forceinline__ int lds_ldi(const void *p) { return *(volatile lds_i32 *)p; }
-__device__ __forceinline__ void lds_sti(void *p, int v) { *(volatile lds_i32 *)p = v; }
+// The LDS image itself is addressed through address-space-3 pointers
+// throughout (a select between two generic pointers costs a null check and a
+// shared-aperture conversion per access).
+#define LDS __attribute__((address_space(3)))
+typedef LDS v4u lds_v4u;
+typedef LDS unsigned lds_u32;
+typedef LDS int lds_i32;
+__device__ __forceinline__ v4u lds_ld(const LDS v4u *p) { return *(volatile const lds_v4u *)p; }
+__device__ __forceinline__ void lds_st(LDS v4u *p, v4u v) { *(volatile lds_v4u *)p = v; }
+__device__ __forceinline__ unsigned lds_ld32(const LDS void *p) { return *(volatile const lds_u32 *)p; }
+__device__ __forceinline__ int lds_ldi(const LDS int *p) { return *(volatile const lds_i32 *)p; }
+__device__ __forceinline__ void lds_sti(LDS int *p, int v) { *(volatile lds_i32 *)p = v; }
 
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
     constexpr int U = WIDE ? kUw : BURG_NARROW_U;  // diagonals per block (progress published per block)
-    PipeLds<W, SWEEP> &sm = *reinterpret_cast<PipeLds<W, SWEEP> *>(pipe_lds_image);
+    LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
@@ -430,7 +435,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const v4u gE = ld_dev(wbox, oE);
             bool prog = false;
             if (wS && g_is_data(gS)) {
-                v4u *slot = &sm.ins[kq][qs & (kNI - 1)];
+                LDS v4u *slot = &sm.ins[kq][qs & (kNI - 1)];
                 if (!l_is_data(lds_ld(slot))) {
                     lds_st(slot, gS);
                     const v4u e = sent_g(((aS / kR) & 1) ^ 1);
@@ -441,7 +446,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 }
             }
             if (wW && g_is_data(gW)) {
-                v4u *slot = &sm.inw[qw & (kRL - 1)][lane];
+                LDS v4u *slot = &sm.inw[qw & (kRL - 1)][lane];
                 if (!l_is_data(lds_ld(slot))) {
                     lds_st(slot, gW);
                     st_dev(wbox, oW, sent_g(((aW / kR) & 1) ^ 1));
@@ -513,7 +518,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     e = e < 0 ? e + L : e;
                     for (; nf[k] < lim; ++nf[k]) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            ring, (__attribute__((address_space(3))) void *)&sm.win[k][nf[k] & (kWin - 1)][0],
+                            ring, (LDS void *)&sm.win[k][nf[k] & (kWin - 1)][0],
                             16, (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
                         e = e + 1 == L ? 0 : e + 1;
                     }
@@ -587,9 +592,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const unsigned nstep = north_dev ? (unsigned)W * G : (unsigned)hcols * 16u;
     const int ncol_real = north_host ? hcols - tj * W : W;  // columns with a halo slot
     const unsigned ncol = north_dev ? G : 16u;
-    v4u(*src_w)[kWave] = k == 0 ? sm.inw : sm.ewe[k - 1];
-    v4u *const my_st = &sm.st[k][0][0];
-    v4u *const my_st0 = &sm.st0[k][0][0];
+    LDS v4u(*src_w)[kWave] = k == 0 ? sm.inw : sm.ewe[k - 1];
+    LDS v4u *const my_st = &sm.st[k][0][0];
+    LDS v4u *const my_st0 = &sm.st0[k][0][0];
     const unsigned Lu = (unsigned)a.L;  // < 2^21 entries (one descriptor)
     unsigned pw = (unsigned)a.origin;
     const v4u lempty = lds_empty_g();
@@ -606,7 +611,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         bool nt;     // sweep: first step of the lane's next trajectory (state reset)
         double src;  // sweep: the column's source term of the step's trajectory
     };
-    auto fetch = [&](int s) -> In {
+    // EDGE: some lane of the block may sit at column 0 or W-1 (west inflow,
+    // east outflow); interior blocks of wide tiles (W >= 128: 64 lanes cover
+    // at most 64 consecutive columns) skip that work altogether
+    typedef std::integral_constant<bool, true> Edge;
+    typedef std::integral_constant<bool, false> Interior;
+    auto fetch = [&](auto edge_tag, int s) -> In {
+        constexpr bool EDGE = decltype(edge_tag)::value;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -627,7 +638,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.xs = lds_ld(&sm.win[k][s & (kWin - 1)][lane]);
         }
         in.cs = sm.cc[k][c];
-        in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
+        if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
+        else in.gw = v4u{0u, 0u, 0u, 0u};
         in.gs = lds_ld((has_south & (s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
         return in;
     };
@@ -650,14 +662,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         if (has_south) {  // lane i checks the inflow of diagonal sb + i
             const int d = sb + lane;
-            const unsigned hi = lds_ld32((const char *)&sm.ins[k][d & (kNI - 1)] + 4);
+            const unsigned hi = lds_ld32((const LDS char *)&sm.ins[k][d & (kNI - 1)] + 4);
             if (any_lane((lane < U) & (d < KW) & (hi == kLdsEmptyHi))) why |= 2u;
         }
         const int ue = (W - 1 - c0) & (W - 1);  // the lane's column W-1 diagonal in the block
         const int te = t0 + ue;
         const bool oe = (ue < U) & ((unsigned)te < (unsigned)KW) & rowok;
         if (east_lds) {
-            const unsigned hi = lds_ld32((const char *)&sm.ewe[k][(te >> LW) & (kRL - 1)][lane] + 4);
+            const unsigned hi = lds_ld32((const LDS char *)&sm.ewe[k][(te >> LW) & (kRL - 1)][lane] + 4);
             if (any_lane(oe & (hi != kLdsEmptyHi))) why |= 4u;
         }
         if (east_glob) {
@@ -677,12 +689,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 
     // one diagonal (no waits: its block was checked); `next` = also read the
     // inputs of diagonal s + 1 (inside the block)
-    auto diagonal = [&](const int s, const bool next, In &in) {
+    auto diagonal = [&](auto edge_tag, const int s, const bool next, In &in) {
+        constexpr bool EDGE = decltype(edge_tag)::value;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
         const bool valid = (unsigned)t < (unsigned)KW;
-        const bool at0 = c == 0, atE = c == W - 1;
+        const bool at0 = EDGE & (c == 0), atE = EDGE & (c == W - 1);
         const bool need_w = has_west & at0 & valid & rowok;
         const bool need_s = has_south & (s < KW);  // wave-uniform (lane 0 consumes)
         const bool out_e = atE & valid & rowok;
@@ -747,13 +760,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
         if constexpr (WIDE) {
-            if (east_lds) lds_st(out_e ? (void *)&sm.ewe[k][q & (kRL - 1)][lane] : (void *)&sm.dump[lane], eo);
+            if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane], eo);
         } else {
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
         }
         // wide tiles issue every store on every diagonal (out-of-range offsets
-        // are dropped): exactly 3 per diagonal, which the vmcnt of done[] counts
-        if (WIDE || east_glob)
+        // are dropped): exactly 3 per edge and 2 per interior diagonal, which
+        // the vmcnt of done[] counts
+        if (EDGE && (WIDE || east_glob))
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
         if (WIDE || has_north) {
             // one store flavour for both targets: sc0 sc1 (system scope) reaches
@@ -767,9 +781,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         // consumed inbound slots back to empty
         if constexpr (WIDE) {
-            if (has_west) lds_st(need_w ? (void *)&src_w[q & (kRL - 1)][lane] : (void *)&sm.dump[lane], lempty);
+            if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane], lempty);
             if (has_south)
-                lds_st((need_s & (lane == 0)) ? (void *)&sm.ins[k][s & (kNI - 1)] : (void *)&sm.dump[lane],
+                lds_st((need_s & (lane == 0)) ? &sm.ins[k][s & (kNI - 1)] : &sm.dump[lane],
                        lempty);
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
@@ -787,7 +801,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
-        if (next) in = fetch(s + 1);
+        if (next) in = fetch(edge_tag, s + 1);
     };
 
     const int total = KW + kWave - 1;
@@ -799,15 +813,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     for (int sb = 0; sb < total; sb += U) {
         if constexpr (WIDE) {
             // every store older than this block's predecessor has completed
-            // (exactly 3 stores per diagonal, no loads): the loader may read
-            // ring entries written before diagonal sb - U
-            // s_waitcnt vmcnt(24) / vmcnt(12) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]
+            // (2 or 3 stores per diagonal, no loads: waiting down to the smaller
+            // count, 2 U, covers both kinds of predecessor): the loader may read
+            // ring entries written before diagonal sb - U.
+            // s_waitcnt vmcnt(16) / vmcnt(8) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]
             // | lgkmcnt[11:8] | vmcnt[5:4] << 14; expcnt / lgkmcnt at their max =
             // no wait).  A builtin, not inline asm: asm would keep the compiler
             // from proving the kernel AGPR-free, and the unused AGPR budget it
             // then reserves caps the waves per SIMD.
-            if constexpr (kUw == 8) __builtin_amdgcn_s_waitcnt((1 << 14) | (0xF << 8) | (7 << 4) | 8);
-            else __builtin_amdgcn_s_waitcnt((0xF << 8) | (7 << 4) | 12);
+            if constexpr (kUw == 8) __builtin_amdgcn_s_waitcnt((1 << 14) | (0xF << 8) | (7 << 4) | 0);
+            else __builtin_amdgcn_s_waitcnt((0xF << 8) | (7 << 4) | 8);
             static_assert(kUw == 8 || kUw == 4, "vmcnt covers one block of stores");
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
@@ -836,9 +851,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             }
             if (aborted) break;
         }
-        in = fetch(sb);
+        const int sm_ = sb & (W - 1);
+        if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
+            in = fetch(Edge(), sb);
 #pragma unroll
-        for (int u = 0; u < U; ++u) diagonal(sb + u, u + 1 < U, in);
+            for (int u = 0; u < U; ++u) diagonal(Edge(), sb + u, u + 1 < U, in);
+        } else {
+            in = fetch(Interior(), sb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) diagonal(Interior(), sb + u, u + 1 < U, in);
+        }
     }
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, spins);
