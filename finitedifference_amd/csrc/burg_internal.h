@@ -73,6 +73,9 @@ struct StreamStats {
                                         // busy, 2 west not written, 3 south not written,
                                         // 4 range (IEEE redo), 5 entries that needed a re-poll
     unsigned long long nonfinite_diagonals;  // diagonals whose new state has a NaN / Inf
+    unsigned long long prof[8];  // pipe, built with -DBURG_PIPE_PROF: compute-wave clocks in
+                                 // [0] the loop, [1] block-start store waits, [2] readiness
+                                 // waits, [4 + k] readiness waits of compute wave k
 };
 
 // Tiling of a slab for the streaming engine: nti strips of 64 rows, ntj tiles

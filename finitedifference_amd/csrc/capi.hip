@@ -324,9 +324,12 @@ void stream_free(burg_ctx *c)
 }
 
 // Pipe engine plan: the narrowest W in {8, 16, ..., 1024} whose tile count
-// fits the target (1024 = one compute wave per SIMD), every workgroup (4
-// tiles + comm wave) resident at once; W <= 16 keeps the previous states in
-// LDS, wider tiles stream them from the HBM ring (pipe.hip).
+// fits the target, every workgroup (4 tiles + comm wave, + loader wave for
+// wide tiles) resident at once; W <= 16 keeps the previous states in LDS,
+// wider tiles stream them from the HBM ring (pipe.hip).  Target (target <= 0:
+// automatic): narrow tiles 1024 (one compute wave per SIMD); wide tiles as
+// many as there are resident compute-wave slots (two per SIMD for W = 64,
+// 128).
 bool pipe_plan(burg_ctx *c, int target, StreamPlan *out, int *nwj)
 {
     std::vector<int> Ws;
@@ -351,7 +354,8 @@ bool pipe_plan(burg_ctx *c, int target, StreamPlan *out, int *nwj)
             pf = p;
             wf = wj;
         }
-        if (p.ntiles <= target) {
+        const int tgt = target > 0 ? target : W <= 16 ? 1024 : 4 * cap;
+        if (p.ntiles <= tgt) {
             *out = p;
             *nwj = wj;
             return true;
@@ -371,7 +375,7 @@ int stream_setup(burg_ctx *c)
         const int target = c->tiles_target_opt > 0 ? c->tiles_target_opt : 1024;
         StreamPlan pp{};
         int wj = 0;
-        if (c->engine == BURG_ENGINE_PIPE && pipe_plan(c, target, &pp, &wj)) {
+        if (c->engine == BURG_ENGINE_PIPE && pipe_plan(c, c->tiles_target_opt, &pp, &wj)) {
             c->sp = pp;
             c->nwj = wj;
             c->eng_eff = BURG_ENGINE_PIPE;
@@ -579,9 +583,23 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         if (const char *e = std::getenv("BURG_STREAM_DEBUG"))  // diagnostics
             if (std::atoi(e) & 8)
                 std::fprintf(stderr,
-                             "[stream] slow-path causes: east-busy %llu north-busy %llu "
-                             "west-unwritten %llu south-unwritten %llu range %llu repoll %llu\n",
+                             c->eng_eff == BURG_ENGINE_PIPE
+                                 ? "[pipe] blocks that waited, by missing kind: east %llu north %llu "
+                                   "west %llu south %llu window %llu; comm polls %llu\n"
+                                 : "[stream] slow-path causes: east-busy %llu north-busy %llu "
+                                   "west-unwritten %llu south-unwritten %llu range %llu repoll %llu\n",
                              ss.why[0], ss.why[1], ss.why[2], ss.why[3], ss.why[4], ss.why[5]);
+        if (const char *e = std::getenv("BURG_STREAM_DEBUG"))
+            if ((std::atoi(e) & 8) && ss.prof[0])
+                std::fprintf(stderr, "[pipe] compute-wave clocks: loop %llu, store waits %llu (%.1f%%), "
+                                     "readiness waits %llu (%.1f%%)\n",
+                             ss.prof[0], ss.prof[1], 100.0 * ss.prof[1] / ss.prof[0], ss.prof[2],
+                             100.0 * ss.prof[2] / ss.prof[0]);
+        if (const char *e = std::getenv("BURG_STREAM_DEBUG"))
+            if ((std::atoi(e) & 8) && ss.prof[0])
+                std::fprintf(stderr, "[pipe] readiness waits by compute wave: %.1f%% %.1f%% %.1f%% %.1f%%\n",
+                             400.0 * ss.prof[4] / ss.prof[0], 400.0 * ss.prof[5] / ss.prof[0],
+                             400.0 * ss.prof[6] / ss.prof[0], 400.0 * ss.prof[7] / ss.prof[0]);
         st->slow_ticks = (int64_t)ss.slow_ticks;
         st->stream_launches = launches;
         st->ieee_diagonals = (int64_t)ss.ieee_diagonals;

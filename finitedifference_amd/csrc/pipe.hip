@@ -93,14 +93,35 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #define BURG_NARROW_U 4
 #endif
 constexpr int kLA = BURG_KLA;  // poll window (diagonals ahead of a compute wave's progress)
-#ifndef BURG_KWIN
-#define BURG_KWIN 16
+// Wide tiles run one workgroup per CU with a 16-diagonal window and blocks of
+// 8.  Built with -DBURG_TWO_PER_CU=1, W = 64 and 128 run two workgroups per CU
+// instead (two compute waves per SIMD: one wave's scalar, LDS and memory
+// instructions issue beside the other's fp64 VALU -- 1.25x the compute rate
+// per SIMD), which leaves 80 KB of LDS per workgroup: a 12-diagonal window,
+// blocks of 4.  Measured at 4096^2 (W = 128, 2048 tiles) the longer
+// hand-off chains then stall 20-27 % of the time and the whole runs slower
+// (118-124 vs 135 Gcell-updates/s for W = 256), so it is off by default.
+#ifndef BURG_TWO_PER_CU
+#define BURG_TWO_PER_CU 0
 #endif
-#ifndef BURG_UW
-#define BURG_UW 8
-#endif
-constexpr int kWin = BURG_KWIN;  // wide tiles: LDS window of previous states per compute wave (diagonals)
-constexpr int kUw = BURG_UW;     // wide tiles: diagonals per block (progress / store completion published)
+template <int W>
+constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
+template <int W>
+constexpr int win_of() { return two_per_cu<W>() ? 12 : 16; }  // window (diagonals)
+template <int W>
+constexpr int uw_of() { return two_per_cu<W>() ? 4 : 8; }  // block (diagonals)
+
+// s_waitcnt vmcnt(N) with expcnt / lgkmcnt at their maximum (no wait): gfx9
+// encoding vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.  A
+// builtin, not inline asm: asm would keep the compiler from proving the
+// kernel AGPR-free, and the AGPR budget it then reserves caps the waves per
+// SIMD.
+template <int N>
+__device__ __forceinline__ void wait_vmcnt()
+{
+    static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt(((N >> 4) << 14) | (0xF << 8) | (7 << 4) | (N & 15));
+}
 
 __device__ __forceinline__ d2 as_d2(v4u v)
 {
@@ -233,7 +254,7 @@ struct PipeLds {
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
     // wide: previous states by diagonal, filled by LDS-DMA -- first in the
     // image: the DMA's LDS address comes from M0[15:0] (the 64 KB below 2^16)
-    v4u win[4][WIDE ? kWin : 1][WIDE ? kWave : 1];
+    v4u win[4][WIDE ? win_of<W>() : 1][WIDE ? kWave : 1];
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
@@ -273,7 +294,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
-    constexpr int U = WIDE ? kUw : BURG_NARROW_U;  // diagonals per block (progress published per block)
+    constexpr int U = WIDE ? uw_of<W>() : BURG_NARROW_U;  // diagonals per block (progress published per block)
+    constexpr int KWIN = win_of<W>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -493,11 +515,15 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
     if (WIDE && wave == 5) {
         // ================= loader wave (wide tiles) =================
-        // window slot d mod kWin of compute wave k <- ring entry (origin +
+        // window slot d mod KWIN of compute wave k <- ring entry (origin +
         // d - W) of its tile, once (1) the slot's previous diagonal is done
-        // (d < prog + kWin), (2) that entry's store has completed
+        // (d < prog + KWIN), (2) that entry's store has completed
         // (d - W < done) -- entries d < W are the initial state, written
-        // before the launch.
+        // before the launch.  One block of U entries per compute wave and
+        // round; the DMAs land in issue order, so each wave's block is
+        // published as soon as it (not the whole round) has landed.  (At a
+        // priority above the compute waves' it would slow the compute wave it
+        // shares a SIMD with, and with it the whole pipeline.)
         __builtin_amdgcn_s_setprio(0);
         // the compute waves run whole blocks of U diagonals
         const int total = (KW + kWave - 1 + U - 1) / U * U;
@@ -505,34 +531,51 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         int nf[4] = {0, 0, 0, 0};
         long long t_prog = now_rt();
         for (;;) {
-            bool left = false, issued = false;
+            bool left = false;
+            int got[4] = {0, 0, 0, 0};  // blocks issued this round, per wave
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k >= nval) continue;
                 const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
-                const int lim = min(min(total, pk + kWin), dk + W);
+                const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
                 if (nf[k] < lim) {
                     const __amdgpu_buffer_rsrc_t ring =
                         rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * L * kWave, (size_t)L * kWave * 16);
                     long long e = (a.origin + nf[k] - W) % L;
                     e = e < 0 ? e + L : e;
-                    for (; nf[k] < lim; ++nf[k]) {
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-                            ring, (LDS void *)&sm.win[k][nf[k] & (kWin - 1)][0],
-                            16, (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
+                    int slot = nf[k] % KWIN;
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
+                                                                 (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
                         e = e + 1 == L ? 0 : e + 1;
+                        slot = slot + 1 == KWIN ? 0 : slot + 1;
                     }
-                    issued = true;
+                    nf[k] += U;
+                    got[k] = 1;
                 }
                 left |= nf[k] < total;
             }
-            if (issued) {
-                __builtin_amdgcn_s_waitcnt(0);  // the DMA rows have landed in LDS
+            const int nb = got[0] + got[1] + got[2] + got[3];
+            if (nb) {
+                // wave k's rows have landed once at most U x (blocks issued
+                // after it) loads are outstanding
+                int after = nb;
 #pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    if (k < nval && lane == 0) lds_sti(&sm.filled[k], nf[k]);
+                for (int k = 0; k < 4; ++k) {
+                    if (!got[k]) continue;
+                    --after;
+                    switch (after) {
+                    case 0: wait_vmcnt<0>(); break;
+                    case 1: wait_vmcnt<U>(); break;
+                    case 2: wait_vmcnt<2 * U>(); break;
+                    default: wait_vmcnt<3 * U>(); break;
+                    }
+                    if (lane == 0) lds_sti(&sm.filled[k], nf[k]);
+                }
                 t_prog = now_rt();
             }
+            const bool issued = nb != 0;
             if (!left || lds_ldi(&sm.perm[5])) break;
             if (!issued) {
                 if (now_rt() - t_prog > a.spin_ticks) {
@@ -600,7 +643,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const v4u lempty = lds_empty_g();
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
-    unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0;
+    unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0, wait_ticks = 0;
+    unsigned wait_why[5] = {0, 0, 0, 0, 0};  // blocks that waited, by first missing kind
     bool aborted = false;
 
 
@@ -635,7 +679,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         } else {
             in.nt = false;
             in.src = 0.0;
-            in.xs = lds_ld(&sm.win[k][s & (kWin - 1)][lane]);
+            in.xs = lds_ld(&sm.win[k][s % KWIN][lane]);
         }
         in.cs = sm.cc[k][c];
         if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
@@ -810,27 +854,36 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // in flight -- into every diagonal.
     __builtin_amdgcn_s_waitcnt(0);
     In in;
+#ifdef BURG_PIPE_PROF
+    unsigned long long pf_vm = 0;
+    const unsigned long long pf0 = __builtin_amdgcn_s_memtime();
+#endif
     for (int sb = 0; sb < total; sb += U) {
+#ifdef BURG_PIPE_PROF
+        const unsigned long long pfa = __builtin_amdgcn_s_memtime();
+#endif
         if constexpr (WIDE) {
             // every store older than this block's predecessor has completed
             // (2 or 3 stores per diagonal, no loads: waiting down to the smaller
             // count, 2 U, covers both kinds of predecessor): the loader may read
-            // ring entries written before diagonal sb - U.
-            // s_waitcnt vmcnt(16) / vmcnt(8) (gfx9 encoding: vmcnt[3:0] | expcnt[6:4]
-            // | lgkmcnt[11:8] | vmcnt[5:4] << 14; expcnt / lgkmcnt at their max =
-            // no wait).  A builtin, not inline asm: asm would keep the compiler
-            // from proving the kernel AGPR-free, and the unused AGPR budget it
-            // then reserves caps the waves per SIMD.
-            if constexpr (kUw == 8) __builtin_amdgcn_s_waitcnt((1 << 14) | (0xF << 8) | (7 << 4) | 0);
-            else __builtin_amdgcn_s_waitcnt((0xF << 8) | (7 << 4) | 8);
-            static_assert(kUw == 8 || kUw == 4, "vmcnt covers one block of stores");
+            // ring entries written before diagonal sb - U
+            wait_vmcnt<2 * U>();
+#ifdef BURG_PIPE_PROF
+            pf_vm += __builtin_amdgcn_s_memtime() - pfa;
+#endif
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
         if (lane == 0) lds_sti(&sm.prog[k], sb);
         unsigned why = block_missing(sb);
         if (__builtin_expect(why != 0, 0)) {
             const long long t0 = now_rt();
+            const unsigned long long c0 = __builtin_amdgcn_s_memtime();
             ++slow_n;
+            wait_why[0] += (why & 12u) != 0;  // east (LDS ring or global grant)
+            wait_why[1] += (why & 16u) != 0;  // north grant
+            wait_why[2] += (why & 1u) != 0;   // west inflow
+            wait_why[3] += (why & 2u) != 0;   // south inflow
+            wait_why[4] += (why & 32u) != 0;  // previous states (loader window)
             for (;;) {
                 ++spins;
                 __builtin_amdgcn_s_sleep(1);
@@ -849,6 +902,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     break;
                 }
             }
+            wait_ticks += __builtin_amdgcn_s_memtime() - c0;
             if (aborted) break;
         }
         const int sm_ = sb & (W - 1);
@@ -867,6 +921,15 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if (slow_n) atomicAdd(&a.stats->slow_diagonals, slow_n);
         if (ieee_n) atomicAdd(&a.stats->ieee_diagonals, ieee_n);
         if (nonfin_n) atomicAdd(&a.stats->nonfinite_diagonals, nonfin_n);
+        if (wait_ticks) atomicAdd(&a.stats->slow_ticks, wait_ticks);
+        for (int i = 0; i < 5; ++i)
+            if (wait_why[i]) atomicAdd(&a.stats->why[i], (unsigned long long)wait_why[i]);
+#ifdef BURG_PIPE_PROF
+        atomicAdd(&a.stats->prof[0], __builtin_amdgcn_s_memtime() - pf0);
+        atomicAdd(&a.stats->prof[1], pf_vm);
+        atomicAdd(&a.stats->prof[2], wait_ticks);
+        atomicAdd(&a.stats->prof[4 + k], wait_ticks);
+#endif
         atomicAdd(&a.stats->tile_steps, (unsigned long long)K);
     }
 }
@@ -934,17 +997,20 @@ bool set_lds_limit(const void *fn, size_t bytes)
     return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess;
 }
 
-int pipe_per_cu_opt()
+// workgroups per CU of the wide-tile engine: one, or two for W = 64, 128 in a
+// -DBURG_TWO_PER_CU=1 build (their LDS image fits twice); BURG_PIPE_WG_PER_CU
+// overrides (tuning knob)
+int pipe_per_cu_opt(int W)
 {
     static int v = -1;
     if (v < 0) {
-        v = 1;
-        if (const char *e = std::getenv("BURG_PIPE_WG_PER_CU")) {  // tuning knob
+        v = 0;
+        if (const char *e = std::getenv("BURG_PIPE_WG_PER_CU")) {
             const int x = std::atoi(e);
             if (x >= 1 && x <= 2) v = x;
         }
     }
-    return v;
+    return v ? v : (BURG_TWO_PER_CU && (W == 64 || W == 128)) ? 2 : 1;
 }
 
 }  // namespace
@@ -962,7 +1028,7 @@ int pipe_max_resident_blocks(int W, bool sweep)
         return -3;
     const void *fn = pipe_fn(W, sweep);
     if (!fn) return -1;
-    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt());
+    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
         hipSuccess)
@@ -977,7 +1043,7 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
     const void *fn = pipe_fn(W, sweep);
     if (!fn) return -1;
-    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt());
+    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return -1;
     // the census counter starts at zero in every launch
     if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;

@@ -32,4 +32,4 @@ a, st = run(1024, 0.05, get_snapshot_params()[:9], 500, 3)
 b, st2 = run(4096, 0.0125, [(5.19, 0.026)], 500, 2)
 print(f"{tag}: 1024^2 sweep {a:.2f} ms ({1024*1024*4500/a/1e6:.0f} Gcell/s)  blocked {st['slow_diagonals']} "
       f"polls {st['comm_polls']} | 4096^2 traj {b:.2f} ms ({4096*4096*500/b/1e6:.0f} Gcell/s) "
-      f"blocked {st2['slow_diagonals']} polls {st2['comm_polls']} W {st2['stream_w']} tiles {st2['stream_tiles']}", flush=True)
+      f"blocked {st2['slow_diagonals']} wait {st2['slow_ticks']/max(1,st2['slow_diagonals']):.0f}clk polls {st2['comm_polls']} W {st2['stream_w']} tiles {st2['stream_tiles']}", flush=True)
