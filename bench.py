@@ -27,9 +27,13 @@ Extra JSON objects: roofline (the march kernel: algorithmic 32 B per
 cell-update = read the previous state u, v + write the new state u, v,
 SURVEY.md section 8(d); per-launch device time from HIP events on the
 library's stream; peak 8 TB/s; traffic from the committed rocprofv3 PMC
-passes, profiles/pmc_traffic.json), cpu_baseline (the oracle's CPU
-restatement, rank 0 at N = 1, bounded sample) and config2_1024 (BASELINE
-configs[1]: the 1024^2 9-mu snapshot sweep).  Only the cpu_baseline leg
+passes, profiles/pmc_traffic.json), issue_roofline (the compute waves'
+instruction-issue floor per diagonal from the kernel ISA, tools/isa_count.py,
+against the measured time per diagonal), cpu_baseline (the oracle's CPU
+restatement, rank 0 at N = 1, bounded sample: the march on every host
+thread, and the reference's Newton on one core), config2_1024 (BASELINE
+configs[1]: the 1024^2 9-mu snapshot sweep) and end_to_end (run_fom.main's
+timed region at 1024^2 x 500: march + D2H + .npy file).  Only the cpu_baseline leg
 touches oracle/.  rom_pipeline: secondary numbers of the reference's ROM
 driver at 250^2 (sweep, POD, LSPG; --no-rom skips).
 """
@@ -80,6 +84,9 @@ def parse():
                          "for the host-side collectives (use small slabs so all ranks' "
                          "workgroups are resident together)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--isa-file", default=os.path.join(ROOT, "profiles", "r02", "pipe_isa.json"))
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end field (1024^2 x 500 trajectory + .npy file)")
     return ap.parse_args()
 
 
@@ -90,26 +97,114 @@ def dist_env():
     return rank, world, local
 
 
+def host_threads():
+    """CPU threads this process may use: the affinity mask, capped by
+    OMP_NUM_THREADS when set (the GPU box sets it to its CPU share)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
 def cpu_baseline(nx, dt, seconds):
-    """Oracle restatement of the reference algorithm (newton_raphson + exact
-    block solve, C/hypernet2D.py:72-131,1811-1857) on the host, 1 thread,
-    first steps of the same trajectory until `seconds` elapse."""
+    """The fastest CPU algorithm of this build on the bench's grid: the
+    oracle's closed-form march (orc_march_sweep, the same arithmetic as the GPU
+    kernel), one trajectory per host thread (the training mu of
+    get_snapshot_params, cycled), OpenMP; steps sized so the sample takes about
+    `seconds`.  Beside it, the reference algorithm itself (newton_raphson +
+    exact block solve, C/hypernet2D.py:72-131,1811-1857) on one core."""
     from oracle import oracle
+    from finitedifference_amd.config import get_snapshot_params
     P = oracle.Problem(nx, dt=dt)
-    w = np.ones(P.m)
+    w0 = np.ones(P.m)
+    thr = host_threads()
+    mus = [get_snapshot_params()[j % 9] for j in range(thr)]
     t0 = time.perf_counter()
-    steps = 0
+    P.march_sweep(w0, mus[:1], 1, 1)  # one step, one thread: sizes the sample
+    t1 = time.perf_counter() - t0
+    steps = max(1, int(seconds / max(t1, 1e-3) / 1.5))
+    t0 = time.perf_counter()
+    used = P.march_sweep(w0, mus, steps, thr)
+    el = time.perf_counter() - t0
+    march = nx * nx * steps * len(mus) / el / 1e6
+    # the reference algorithm, one core, a short sample
+    w = w0
+    t0 = time.perf_counter()
+    nsteps = 0
     while True:
         w, its, rel = P.newton_step(w)
-        steps += 1
-        if time.perf_counter() - t0 >= seconds:
+        nsteps += 1
+        if time.perf_counter() - t0 >= min(seconds, 6.0):
             break
-    el = time.perf_counter() - t0
-    return {"value": nx * nx * steps / el / 1e6, "unit": "Mcell-updates/s", "cores": 1,
+    eln = time.perf_counter() - t0
+    return {"value": round(march, 3), "unit": "Mcell-updates/s", "cores": int(used),
             "kind": "port", "nproc": os.cpu_count(),
-            "sample": f"oracle Newton (reference algorithm, exact block solve in place of "
-                      f"SuperLU) on {nx}x{nx}, dt={dt:g}, first {steps} of the 500 steps from "
-                      f"w0=1, {el:.1f} s, 1 thread"}
+            "sample": f"oracle march (orc_march_sweep, OpenMP) on {nx}x{nx}, dt={dt:g}: {len(mus)} "
+                      f"trajectories (training mu) x {steps} steps from w0=1, one per thread, "
+                      f"{el:.1f} s on {used} threads",
+            "newton_1core": {"value": round(nx * nx * nsteps / eln / 1e6, 3),
+                             "unit": "Mcell-updates/s", "cores": 1,
+                             "sample": f"oracle Newton (reference algorithm, exact block solve in "
+                                       f"place of SuperLU), first {nsteps} of the 500 steps, "
+                                       f"{eln:.1f} s"}}
+
+
+def end_to_end(nx=1024, T=500):
+    """C/run_fom.py:41-43's timed region on the GPU: one {nx}^2 x {T}
+    trajectory from w0 = 1 (dt = 0.05, mu = (5.19, 0.026)) including the
+    snapshot matrix's device-to-host copy and its .npy file (burg_run_npy:
+    pinned double-buffered writer), wall clock of the call; the file goes to
+    a temporary directory and is deleted."""
+    import tempfile
+    from finitedifference_amd.solver import FOMContext
+    ctx = FOMContext(nx, nx, engine="pipe")
+    g = np.linspace(0, 100, nx + 1)
+    ctx.set_problem(g, g, DT, MU)
+    d = tempfile.mkdtemp(prefix="burg_e2e_")
+    path = os.path.join(d, "snaps.npy")
+    try:
+        t0 = time.perf_counter()
+        st = ctx.run_to_npy(np.ones(ctx.m), T, path)
+        wall = time.perf_counter() - t0
+        size = os.path.getsize(path)
+        hdr = np.load(path, mmap_mode="r").shape
+    except OSError as e:
+        return {"error": f"{type(e).__name__}: {e}"}
+    finally:
+        ctx.close()
+        if os.path.exists(path):
+            os.remove(path)
+        os.rmdir(d)
+    return {"grid": f"{nx}x{nx}", "time_steps": T, "wall_s": round(wall, 3),
+            "value": round(nx * nx * T / wall / 1e6, 3), "unit": "Mcell-updates/s",
+            "march_kernel_ms": round(st["loop_ms"], 3), "file_bytes": size, "npy_shape": list(hdr),
+            "what": "run_fom.main's timed region: march + D2H + np.save of the (2n, T+1) snapshot "
+                    "matrix (burg_run_npy)"}
+
+
+def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=2.4):
+    """Issue bound of the march kernel's compute waves: instructions per
+    diagonal from the kernel's ISA (tools/isa_count.py -> profiles/r02/
+    pipe_isa.json) at 4 cycles each (+12 per fp64 transcendental: one wave
+    per SIMD issues at most one instruction per 4 cycles, tools/probes/
+    issue_probe.hip), against the measured time per diagonal at the nominal
+    2.4 GHz clock.  Wide tiles mix interior and edge blocks ((64/U + 1) of
+    every W/U blocks are edge blocks)."""
+    try:
+        d = json.load(open(isa_file))[kname]["per_diagonal_averages"]
+    except Exception:
+        return None
+    if "interior_block" in d:
+        fe = min(1.0, (64 / U + 1) / (W / U)) if W >= 128 else 1.0
+        cyc = (1 - fe) * d["interior_block"]["issue_cycles"] + fe * d["edge_block"]["issue_cycles"]
+        ins = (1 - fe) * d["interior_block"]["total"] + fe * d["edge_block"]["total"]
+    else:
+        cyc, ins = d["block"]["issue_cycles"], d["block"]["total"]
+    meas = avg_ms * 1e6 / diagonals * clock_ghz
+    return {"bound": "issue", "instructions_per_diagonal": round(ins, 1),
+            "issue_cycles_per_diagonal": round(cyc, 1),
+            "measured_cycles_per_diagonal": round(meas, 1), "frac": round(cyc / meas, 4),
+            "clock_ghz": clock_ghz, "diagonals_per_wave": diagonals,
+            "source": os.path.relpath(isa_file, ROOT)}
 
 
 def stencil_roofline(nx, reps=20, pmc_file=None):
@@ -313,8 +408,15 @@ def main():
                 "traffic_source": tsrc,
             },
         }
+        if st["engine"] == 2:
+            iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + 63, args.isa_file,
+                                 st["stream_w"], U=8 if st["stream_w"] > 16 else 4)
+            if iss:
+                out["issue_roofline"] = iss
         if world == 1 and not args.no_1024:
-            out["config2_1024"] = config2_1024(args.pmc_file)
+            out["config2_1024"] = config2_1024(args.pmc_file, args.isa_file)
+        if world == 1 and not args.no_e2e:
+            out["end_to_end"] = end_to_end()
         if world == 1 and args.stencil_nx > 0:
             out["stencil_roofline"] = stencil_roofline(args.stencil_nx, pmc_file=args.pmc_file)
         if world == 1 and not args.no_rom:
@@ -327,7 +429,7 @@ def main():
         dist.destroy_process_group()
 
 
-def config2_1024(pmc_file, steps=3):
+def config2_1024(pmc_file, isa_file=None, steps=3):
     """BASELINE configs[1] (1024^2, dt = 0.05 as run_fom.py): the 9-mu FOM
     snapshot sweep in one burg_sweep launch (pipe_kernel<16, true>), every
     state kept in HBM; secondary to the headline."""
@@ -351,9 +453,13 @@ def config2_1024(pmc_file, steps=3):
     ms = kern / steps
     gbs = BYTES_PER_CELL_UPDATE * upd / (ms * 1e-3) / 1e9
     traffic, tsrc = read_pmc(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
+    kname = f"pipe_kernel<{st['stream_w']}, true>"
+    iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 63, isa_file, st["stream_w"],
+                         U=8 if st["stream_w"] > 16 else 4) if isa_file else None
     return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
+            "issue_roofline": iss,
             "value": round(upd * steps / el / 1e6, 3), "unit": "Mcell-updates/s",
-            "kernel": f"pipe_kernel<{st['stream_w']}, true>", "avg_launch_ms": round(ms, 4),
+            "kernel": kname, "avg_launch_ms": round(ms, 4),
             "roofline_frac": round(gbs / HBM_PEAK_GBS, 5), "achieved_GBs": round(gbs, 1),
             "ieee_diagonals": st["ieee_diagonals"], "traffic": traffic, "traffic_source": tsrc}
 
