@@ -354,6 +354,11 @@ def main():
     value = cells * T * nmu * args.steps / elapsed / 1e6
 
     st_main = st
+    halo = None
+    if world > 1:
+        hin, hout = ctx.halo_modes()
+        halo = {0: None, 1: "pinned host memory", 2: "consumer GPU memory over IPC (xGMI)"}[
+            hout if rank == 0 else hin]
     ctx.close()  # give the trajectory ring back before the secondary probes
     if rank == 0:
         st = st_main
@@ -392,6 +397,7 @@ def main():
                 "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T, "dt": dt,
                 "trajectories_per_step": nmu,
                 "parallelism": f"row-slab x{world}",
+                "halo_ring": halo,
             },
             "engine": {"name": eng, "tile_w": st["stream_w"], "tiles": st["stream_tiles"],
                        "blocked_diagonals": st["slow_diagonals"],

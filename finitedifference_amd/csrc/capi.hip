@@ -135,10 +135,15 @@ struct burg_ctx {
     const d2 *ov_colc = nullptr;
     const double *ov_lbc = nullptr;
     long long spin_ticks = 500000000LL;  // 5 s of s_memrealtime (100 MHz)
-    // multi-GPU halo rings (pinned shared host memory)
+    // multi-GPU halo rings: the consumer's device memory
+    // over IPC (mode 2), or pinned shared host memory (mode 1)
     std::string halo_name;
-    void *halo_in_host = nullptr, *halo_out_host = nullptr;
-    d2 *halo_in_dev = nullptr, *halo_out_dev = nullptr;
+    void *halo_in_host = nullptr, *halo_out_host = nullptr;  // shm objects (ring + control page)
+    d2 *halo_in_hostdev = nullptr, *halo_out_hostdev = nullptr;  // their device mappings
+    d2 *halo_in_ring = nullptr;   // consumer: its device ring (uncached, exported)
+    void *halo_out_ipc = nullptr;  // producer: the neighbour's device ring, opened
+    d2 *halo_in_dev = nullptr, *halo_out_dev = nullptr;  // what the kernel uses
+    int halo_in_mode = 0, halo_out_mode = 0;             // 0 unknown, 1 host, 2 device
     size_t halo_bytes = 0;
     bool halo_connected = false;
 
@@ -311,6 +316,8 @@ int read_stats(burg_ctx *c, burg_stats *st)
     return 0;
 }
 
+int halo_resolve_in(burg_ctx *c);  // multi-GPU halo rings (below)
+
 // ---- streaming engine -------------------------------------------------------
 void stream_free(burg_ctx *c)
 {
@@ -430,6 +437,7 @@ int stream_setup(burg_ctx *c)
     }
     if (c->world > 1 && !c->halo_connected)
         return fail(BURG_ESTATE, "slab context not connected (burg_slab_connect) to its neighbours");
+    if (c->world > 1) CHK(halo_resolve_in(c));
     if (!c->colc_ready) {
         CHK(launch_colc(c->cf, c->sp.ntj * c->sp.W, c->d_colc, c->stream));
         c->colc_ready = true;
@@ -831,18 +839,48 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
 
 // ---- multi-GPU halo rings ------------------------------------------------
 // One ring per rank boundary b (between ranks b-1 and b): kPipeR step slots x
-// nx granules of 16 B in POSIX shared memory, created and initialised (all
-// slots: sentinel colour 0) by the consumer rank b, attached by the producer
-// rank b-1, pinned and mapped into each GPU's address space.  Both GPUs reach
-// it at system scope; no host thread touches it at run time.
+// nx granules of 16 B, all sentinel colour 0 at creation, written by the
+// producer rank b-1's top strip and polled by the consumer rank b's comm
+// waves, both at system scope (sc0 sc1); no host thread touches it at run
+// time.  Where it lives:
+//   * mode 2 (default): the consumer's own device memory -- uncached
+//     (hipDeviceMallocUncached: remote stores arriving over xGMI are seen by
+//     the polls without an L2 invalidate), exported with hipIpcGetMemHandle
+//     and opened by the producer (hipIpcOpenMemHandle): producer stores cross
+//     xGMI once, consumer polls stay on its own HBM;
+//   * mode 1: pinned POSIX shared host memory mapped into both GPUs (the
+//     fallback, and BURG_HALO=host).
+// Rendezvous: a POSIX shared-memory object per boundary, created by the
+// consumer: the host ring followed by a control page (the IPC handle, whether
+// the device ring exists, and the mode the producer chose when it connected).
+// The consumer reads the producer's choice at its first launch.
+struct HaloCtl {
+    uint32_t magic;
+    uint32_t dev_ok;  // consumer: device ring exported
+    volatile uint32_t choice;  // producer: 1 host ring, 2 device ring
+    uint32_t pad;
+    hipIpcMemHandle_t handle;
+};
+constexpr uint32_t kHaloMagic = 0xB0A6C7A1u;
+constexpr size_t kHaloCtlBytes = 4096;
+static_assert(sizeof(HaloCtl) <= kHaloCtlBytes, "halo control page");
+
 std::string halo_shm_name(const std::string &job, int boundary)
 {
     return "/burg_" + job + "_b" + std::to_string(boundary);
 }
 
+HaloCtl *halo_ctl(const burg_ctx *c, void *host) { return (HaloCtl *)((char *)host + c->halo_bytes); }
+
+bool halo_force_host()
+{
+    const char *e = std::getenv("BURG_HALO");
+    return e && std::strcmp(e, "host") == 0;
+}
+
 int halo_map(burg_ctx *c, const std::string &name, bool create, void **host, d2 **dev)
 {
-    const size_t bytes = c->halo_bytes;
+    const size_t bytes = c->halo_bytes + kHaloCtlBytes;
     const int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
     if (fd < 0) return fail(BURG_EHALO, "shm_open(%s): %s", name.c_str(), strerror(errno));
     if (create && ftruncate(fd, (off_t)bytes) != 0) {
@@ -856,10 +894,11 @@ int halo_map(burg_ctx *c, const std::string &name, bool create, void **host, d2 
     if (create) {
         // sentinel colour 0 (pipe.hip): {lo 0xBEEF5A5A, hi 0x7FF4DEAD} in both halves
         uint32_t *w = (uint32_t *)p;
-        for (size_t i = 0; i < bytes / 4; i += 2) {
+        for (size_t i = 0; i < c->halo_bytes / 4; i += 2) {
             w[i] = 0xBEEF5A5Au;
             w[i + 1] = 0x7FF4DEADu;
         }
+        std::memset((char *)p + c->halo_bytes, 0, kHaloCtlBytes);
     }
     hipError_t e = hipHostRegister(p, bytes, hipHostRegisterMapped);
     if (e != hipSuccess) {
@@ -883,10 +922,52 @@ void halo_unmap(burg_ctx *c, void *&host, d2 *&dev)
 {
     if (host) {
         (void)hipHostUnregister(host);
-        munmap(host, c->halo_bytes);
+        munmap(host, c->halo_bytes + kHaloCtlBytes);
     }
     host = nullptr;
     dev = nullptr;
+}
+
+// consumer: the device ring in its own memory, exported for the producer
+// (any failure leaves the host ring as the only option)
+void halo_export_device_ring(burg_ctx *c, HaloCtl *ctl)
+{
+    if (halo_force_host()) return;
+    void *r = nullptr;
+    if (hipExtMallocWithFlags(&r, c->halo_bytes, hipDeviceMallocUncached) != hipSuccess || !r) {
+        (void)hipGetLastError();
+        return;
+    }
+    hipIpcMemHandle_t h{};
+    if (launch_pipe_fill(r, c->halo_bytes / 16, 0, c->stream) != 0 ||
+        hipStreamSynchronize(c->stream) != hipSuccess || hipIpcGetMemHandle(&h, r) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(r);
+        return;
+    }
+    c->halo_in_ring = (d2 *)r;
+    ctl->handle = h;
+    ctl->dev_ok = 1;
+}
+
+// consumer, first launch after the barrier that follows every rank's
+// burg_slab_connect: take the ring the producer chose
+int halo_resolve_in(burg_ctx *c)
+{
+    if (c->rank == 0 || c->halo_in_mode) return 0;
+    HaloCtl *ctl = halo_ctl(c, c->halo_in_host);
+    const uint32_t ch = ctl->choice;
+    if (ch == 2 && c->halo_in_ring) {
+        c->halo_in_dev = c->halo_in_ring;
+    } else if (ch == 1) {
+        c->halo_in_dev = c->halo_in_hostdev;
+    } else {
+        return fail(BURG_ESTATE, "rank %d: the rank below has not connected to the halo ring yet "
+                                 "(burg_slab_connect on every rank, then a barrier, before the "
+                                 "first launch)", c->rank);
+    }
+    c->halo_in_mode = (int)ch;
+    return 0;
 }
 
 }  // namespace
@@ -961,15 +1042,27 @@ int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows, 
         c->halo_bytes = (size_t)kPipeR * nx * sizeof(d2);
         if (rank > 0) {
             const std::string nm = halo_shm_name(c->halo_name, rank);
-            if ((e = halo_map(c, nm, true, &c->halo_in_host, &c->halo_in_dev))) {
+            if ((e = halo_map(c, nm, true, &c->halo_in_host, &c->halo_in_hostdev))) {
                 burg_ctx_destroy(c);
                 return e;
             }
+            HaloCtl *ctl = halo_ctl(c, c->halo_in_host);
+            halo_export_device_ring(c, ctl);
+            __atomic_store_n(&ctl->magic, kHaloMagic, __ATOMIC_RELEASE);
         }
     } else {
         c->halo_connected = true;
     }
     *out = c;
+    return BURG_OK;
+}
+
+int burg_slab_halo_mode(burg_ctx *c, int *in_mode, int *out_mode)
+{
+    if (!c || !in_mode || !out_mode) return fail(BURG_EINVAL, "null argument");
+    if (c->world > 1 && c->halo_connected) CHK(halo_resolve_in(c));
+    *in_mode = c->rank > 0 ? c->halo_in_mode : 0;
+    *out_mode = c->rank + 1 < c->world ? c->halo_out_mode : 0;
     return BURG_OK;
 }
 
@@ -980,7 +1073,25 @@ int burg_slab_connect(burg_ctx *c)
     HIPCHK(hipSetDevice(c->device));
     if (c->rank + 1 < c->world) {
         const std::string nm = halo_shm_name(c->halo_name, c->rank + 1);
-        if (int e = halo_map(c, nm, false, &c->halo_out_host, &c->halo_out_dev)) return e;
+        if (int e = halo_map(c, nm, false, &c->halo_out_host, &c->halo_out_hostdev)) return e;
+        HaloCtl *ctl = halo_ctl(c, c->halo_out_host);
+        if (__atomic_load_n(&ctl->magic, __ATOMIC_ACQUIRE) != kHaloMagic)
+            return fail(BURG_EHALO, "halo ring %s: the rank above has not finished creating it",
+                        nm.c_str());
+        uint32_t choice = 1;
+        c->halo_out_dev = c->halo_out_hostdev;
+        if (ctl->dev_ok && !halo_force_host()) {
+            void *p = nullptr;
+            if (hipIpcOpenMemHandle(&p, ctl->handle, hipIpcMemLazyEnablePeerAccess) == hipSuccess && p) {
+                c->halo_out_ipc = p;
+                c->halo_out_dev = (d2 *)p;
+                choice = 2;
+            } else {
+                (void)hipGetLastError();  // fall back to the host ring
+            }
+        }
+        c->halo_out_mode = (int)choice;
+        __atomic_store_n(&ctl->choice, choice, __ATOMIC_RELEASE);
     }
     c->halo_connected = true;
     return BURG_OK;
@@ -1009,8 +1120,10 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_partials);
     dfree(c->d_sumsq);
     stream_free(c);
-    halo_unmap(c, c->halo_in_host, c->halo_in_dev);
-    halo_unmap(c, c->halo_out_host, c->halo_out_dev);
+    if (c->halo_out_ipc) (void)hipIpcCloseMemHandle(c->halo_out_ipc);
+    if (c->halo_in_ring) (void)hipFree(c->halo_in_ring);
+    halo_unmap(c, c->halo_in_host, c->halo_in_hostdev);
+    halo_unmap(c, c->halo_out_host, c->halo_out_hostdev);
     if (c->world > 1 && c->rank > 0) shm_unlink(halo_shm_name(c->halo_name, c->rank).c_str());
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -47,6 +47,14 @@ class FOMContext:
     def connect(self):
         _lib.check(self._L.burg_slab_connect(self._h))
 
+    def halo_modes(self):
+        """(in, out) halo ring placement of a slab context: 0 none (end rank),
+        1 pinned host memory, 2 the consumer GPU's device memory (IPC).  The
+        inbound mode is known once the rank below has connected."""
+        a, b = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self._L.burg_slab_halo_mode(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
     @property
     def m(self):
         return 2 * self.nx * self.ny

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 7
+#define BURG_ABI_VERSION 8
 
 enum burg_status {
     BURG_OK = 0,
@@ -118,15 +118,23 @@ int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);
 /* Multi-GPU (one process per GPU): this rank owns global rows
  * [row0, row0 + nrows) of an nx x ny_total grid (rank 0 the bottom slab).
  * The slabs exchange the one-way halo (north outflow of a slab's top row ->
- * south inflow of the next slab) through rings in POSIX shared memory named
- * from `halo_name` (the same job-unique string on every rank, 1-64 chars),
- * which each GPU reads and writes directly while the time loop runs.  This
- * call creates the ring this rank consumes; after EVERY rank has created its
- * context (a host barrier), call burg_slab_connect to attach the ring this
- * rank produces into.  world == 1 behaves as burg_ctx_create. */
+ * south inflow of the next slab) through a ring each GPU reads or writes
+ * directly while the time loop runs: by default in the consumer's device
+ * memory, opened by the producer over IPC (stores cross xGMI); pinned POSIX
+ * shared host memory when that is unavailable or BURG_HALO=host.  The rings
+ * are found through POSIX shared-memory objects named from `halo_name` (the
+ * same job-unique string on every rank, 1-64 chars).  This call creates the
+ * ring this rank consumes; after EVERY rank has created its context (a host
+ * barrier), call burg_slab_connect to attach the ring this rank produces
+ * into, and run a second barrier before the first launch.  world == 1
+ * behaves as burg_ctx_create. */
 int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows,
                          int rank, int world, const char *halo_name, burg_ctx **out);
 int burg_slab_connect(burg_ctx *ctx);
+/* Where the halo rings live: *in_mode for the ring this rank consumes,
+ * *out_mode for the one it produces into: 0 none (end rank), 1 pinned host
+ * memory, 2 the consumer GPU's device memory (IPC). */
+int burg_slab_halo_mode(burg_ctx *ctx, int *in_mode, int *out_mode);
 
 void burg_ctx_destroy(burg_ctx *ctx);
 

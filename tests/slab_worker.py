@@ -5,7 +5,8 @@ rendezvous over gloo; writes its slab snapshot matrix.
     slab_worker.py N T OUTDIR [run|sweep]
     env: SLAB_NY (rows, default N), SLAB_W (pipe tile width, 0 = plan),
          SLAB_TILES (tiles target per rank), SLAB_SNAP_EVERY (default 1),
-         SLAB_DT (default 0.05)
+         SLAB_DT (default 0.05); writes slab{rank}.npy, .w (tile width) and
+         .halo (halo ring placement: in, out; 1 host, 2 device)
 """
 import os
 import sys
@@ -48,6 +49,8 @@ def main():
         np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
     with open(os.path.join(out, f"slab{rank}.w"), "w") as f:
         f.write(str(st["stream_w"]))
+    with open(os.path.join(out, f"slab{rank}.halo"), "w") as f:
+        f.write("%d %d" % ctx.halo_modes())
     dist.barrier()
     ctx.close()
     dist.destroy_process_group()

@@ -337,27 +337,25 @@ def test_pipe_and_stream_engines_agree(gpu):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("N,world,T", [(128, 2, 9), (150, 3, 7)])
-def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T):
+def _halo_modes(tmp_path, world):
+    """(in, out) halo ring placement each slab worker reported."""
+    return [tuple(int(x) for x in open(os.path.join(tmp_path, f"slab{r}.halo")).read().split())
+            for r in range(world)]
+
+
+@pytest.mark.parametrize("N,world,T,halo", [(128, 2, 9, "device"), (150, 3, 7, "device"),
+                                            (150, 3, 7, "host")])
+def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T, halo):
     """Multi-GPU path, rehearsed on one GPU: `world` processes, one slab each,
-    all on device 0, exchanging the halo through the shared host rings while
-    their time loops run concurrently.  The assembled trajectory is the
-    single-grid sequential march bit for bit."""
-    import subprocess
-    import sys
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    worker = os.path.join(os.path.dirname(__file__), "slab_worker.py")
-    procs = []
-    for r in range(world):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20")
-        procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path)],
-                                      env=env))
-    codes = [p.wait(timeout=110) for p in procs]
-    assert codes == [0] * world, codes
+    all on device 0, exchanging the halo while their time loops run
+    concurrently -- through each consumer's device-memory ring opened over IPC
+    (the default), or the pinned host rings (BURG_HALO=host).  The assembled
+    trajectory is the single-grid sequential march bit for bit."""
+    env = {} if halo == "device" else {"BURG_HALO": "host"}
+    _run_slabs(tmp_path, N, T, world, **env)
+    mode = 2 if halo == "device" else 1
+    want = [(0 if r == 0 else mode, 0 if r == world - 1 else mode) for r in range(world)]
+    assert _halo_modes(tmp_path, world) == want
     from finitedifference_amd.dist import assemble_snaps
     parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
     snaps = assemble_snaps(parts, N, N)
@@ -370,22 +368,8 @@ def test_slab_halo_sweep_two_processes_one_gpu(gpu, orc, tmp_path):
     """The multi-GPU halo stream carries a mu sweep too: 2 slab processes on
     one GPU, 3 trajectories back to back; each assembled trajectory is the
     single-grid march for its mu, bit for bit."""
-    import subprocess
-    import sys
-    import socket
     N, T, world = 128, 6, 2
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    worker = os.path.join(os.path.dirname(__file__), "slab_worker.py")
-    procs = []
-    for r in range(world):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20")
-        procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path),
-                                       "sweep"], env=env))
-    codes = [p.wait(timeout=110) for p in procs]
-    assert codes == [0] * world, codes
+    _run_slabs(tmp_path, N, T, world, mode="sweep")
     from finitedifference_amd.dist import assemble_snaps
     from slab_worker import SWEEP_MUS
     for j, mu in enumerate(SWEEP_MUS):
@@ -398,7 +382,8 @@ def test_slab_halo_sweep_two_processes_one_gpu(gpu, orc, tmp_path):
 
 def _run_slabs(tmp_path, N, T, world, mode="run", timeout=110, **env_extra):
     """Start `world` slab_worker processes on device 0 (gloo rendezvous) and
-    wait for them; env_extra: SLAB_NY, SLAB_W, SLAB_TILES, SLAB_SNAP_EVERY."""
+    wait for them; env_extra: SLAB_NY, SLAB_W, SLAB_TILES, SLAB_SNAP_EVERY,
+    BURG_HALO."""
     import subprocess
     import sys
     import socket
