@@ -194,9 +194,11 @@ def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=2.4):
     except Exception:
         return None
     if "interior_block" in d:
+        # interior blocks of full strips run the steady variant when built
+        inner = d.get("steady_block", d["interior_block"])
         fe = min(1.0, (64 / U + 1) / (W / U)) if W >= 128 else 1.0
-        cyc = (1 - fe) * d["interior_block"]["issue_cycles"] + fe * d["edge_block"]["issue_cycles"]
-        ins = (1 - fe) * d["interior_block"]["total"] + fe * d["edge_block"]["total"]
+        cyc = (1 - fe) * inner["issue_cycles"] + fe * d["edge_block"]["issue_cycles"]
+        ins = (1 - fe) * inner["total"] + fe * d["edge_block"]["total"]
     else:
         cyc, ins = d["block"]["issue_cycles"], d["block"]["total"]
     meas = avg_ms * 1e6 / diagonals * clock_ghz

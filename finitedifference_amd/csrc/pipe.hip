@@ -202,6 +202,16 @@ __device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t rs, unsigned off, 
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 17);
 }
+// the same stores with a scalar offset part (soffset): a per-lane offset that
+// stays constant over a block, a per-diagonal one in an SGPR
+__device__ __forceinline__ void st_dev_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 16);
+}
+__device__ __forceinline__ void st_sys_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 17);
+}
 __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
@@ -658,10 +668,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // EDGE: some lane of the block may sit at column 0 or W-1 (west inflow,
     // east outflow); interior blocks of wide tiles (W >= 128: 64 lanes cover
     // at most 64 consecutive columns) skip that work altogether
-    typedef std::integral_constant<bool, true> Edge;
-    typedef std::integral_constant<bool, false> Interior;
+    // STEADY: an interior block of a full strip with every lane inside the
+    // launch's time range, no ring wrap and no north-column wrap in the block
+    // -- no validity masks, ring and north store offsets in SGPRs
+    typedef std::integral_constant<int, 0> Edge;
+    typedef std::integral_constant<int, 1> Interior;
+    typedef std::integral_constant<int, 2> Steady;
+    unsigned noffs = 0;  // steady blocks: the top lane's north slot offset at the current diagonal
     auto fetch = [&](auto edge_tag, int s) -> In {
-        constexpr bool EDGE = decltype(edge_tag)::value;
+        constexpr bool EDGE = decltype(edge_tag)::value == 0;
+        constexpr bool STEADY = decltype(edge_tag)::value == 2;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -684,7 +700,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         in.cs = sm.cc[k][c];
         if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
         else in.gw = v4u{0u, 0u, 0u, 0u};
-        in.gs = lds_ld((has_south & (s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
+        in.gs = lds_ld((has_south & (STEADY || s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
         return in;
     };
 
@@ -734,14 +750,15 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // one diagonal (no waits: its block was checked); `next` = also read the
     // inputs of diagonal s + 1 (inside the block)
     auto diagonal = [&](auto edge_tag, const int s, const bool next, In &in) {
-        constexpr bool EDGE = decltype(edge_tag)::value;
+        constexpr bool EDGE = decltype(edge_tag)::value == 0;
+        constexpr bool STEADY = decltype(edge_tag)::value == 2;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
-        const bool valid = (unsigned)t < (unsigned)KW;
+        const bool valid = STEADY || (unsigned)t < (unsigned)KW;
         const bool at0 = EDGE & (c == 0), atE = EDGE & (c == W - 1);
         const bool need_w = has_west & at0 & valid & rowok;
-        const bool need_s = has_south & (s < KW);  // wave-uniform (lane 0 consumes)
+        const bool need_s = has_south & (STEADY || s < KW);  // wave-uniform (lane 0 consumes)
         const bool out_e = atE & valid & rowok;
         const bool out_n = (lane == top) & valid & has_north;
         // ---- inflow-independent part of the cell (MarchCell::pre, same op order)
@@ -796,9 +813,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // wide tiles: the loader wave reads this entry back (sc1 DMA) W
         // diagonals later, so it is stored write-through to L2 (sc1): the
         // store's vmcnt then completes at L2, which the done[] protocol needs
-        if constexpr (WIDE) st_dev(ring, valid ? pw * 1024u + lane16 : kOOB, out);
-        else st_plain(ring, valid ? pw * 1024u + lane16 : kOOB, out);
-        pw = pw + 1 == Lu ? 0u : pw + 1;
+        if constexpr (STEADY) {
+            st_dev_so(ring, lane16, pw * 1024u, out);
+            ++pw;  // (no wrap inside a steady block)
+        } else {
+            if constexpr (WIDE) st_dev(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+            else st_plain(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+            pw = pw + 1 == Lu ? 0u : pw + 1;
+        }
         const v4u eo = as_v4u(oe0, oe1);
         const int aq = a.qbase + q;
         // (LDS writes go to a selected address -- a dump slot for lanes
@@ -818,10 +840,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // the host / peer halo ring and is write-through like sc1 for the
             // device mailboxes (consumers poll with sc1 / sc0 sc1 loads)
             const v4u no = as_v4u(on0, on1);
-            const unsigned off = (out_n & (c < ncol_real))
-                                     ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
-                                     : kOOB;
-            st_sys(nrs, off, no);
+            if constexpr (STEADY) {
+                // the top lane's slot: SGPR offset, advanced one column per diagonal
+                st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, noffs, no);
+                noffs += ncol;
+            } else {
+                const unsigned off = (out_n & (c < ncol_real))
+                                         ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
+                                         : kOOB;
+                st_sys(nrs, off, no);
+            }
         }
         // consumed inbound slots back to empty
         if constexpr (WIDE) {
@@ -906,10 +934,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (aborted) break;
         }
         const int sm_ = sb & (W - 1);
+        const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
             in = fetch(Edge(), sb);
 #pragma unroll
             for (int u = 0; u < U; ++u) diagonal(Edge(), sb + u, u + 1 < U, in);
+        } else if (nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
+                   ct0 + U <= ncol_real) {
+            noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
+            in = fetch(Steady(), sb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) diagonal(Steady(), sb + u, u + 1 < U, in);
         } else {
             in = fetch(Interior(), sb);
 #pragma unroll

@@ -103,8 +103,9 @@ def main():
         U = 8 if W > 16 else 4  # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U)
         rr = [r[i:i + U] for r in runs(kernel_body(asm, W, sweep)) for i in range(0, len(r), U)]
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
-        # wide tiles: interior and edge block variants (interior the shorter)
-        names = ["block"] if len(rr) == 1 else ["interior_block", "edge_block"]
+        # wide tiles: steady / interior / edge block variants, shortest first
+        names = {1: ["block"], 2: ["interior_block", "edge_block"],
+                 3: ["steady_block", "interior_block", "edge_block"]}[len(rr)]
         res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}>"] = {
             "per_diagonal_averages": {nm: summarise(r) for nm, r in zip(names, rr)}}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
