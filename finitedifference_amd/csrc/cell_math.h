@@ -129,16 +129,23 @@ struct MarchCell {
         const double q = 0.25 + mm;
         double s, nu, nv;
         if constexpr (FAST) {
-            // operands +0 or of magnitude in [2^-900, 2^900]: div2_normal's exact
-            // range (-0 would come out +0; NaN fails too: the streaming engines
-            // rely on it).  q > 0: q = 0.25 + mm is either <= 0 or >= 2^-55
-            // (Sterbenz), and sqrt_normal is exact there; a zero or negative
-            // discriminant goes to the IEEE path, which reports a NaN.
-            // Bitwise & / |: no short-circuit branches on the critical path.
-            const double au = fabs(cu), av = fabs(cv);
-            range_ok = (((au >= 0x1p-900) & (au <= 0x1p+900)) | (__double_as_longlong(cu) == 0)) &
-                       (((av >= 0x1p-900) & (av <= 0x1p+900)) | (__double_as_longlong(cv) == 0)) &
-                       (q > 0.0);
+            // Cu, Cv of magnitude in [2^-900, 2^900): div2_normal's exact range;
+            // q in [2^-900, 2^900) and positive: sqrt_normal's (q = 0.25 + mm is
+            // either <= 0 or >= 2^-55 by Sterbenz, so this is q > 0 short of
+            // overflow).  Zeros, -0 (it would come out +0), denormals, Inf and
+            // NaN fail and go to the IEEE path, which reports a NaN.  Tested on
+            // the exponent fields of the high words: subtracting 123 << 20 and
+            // extracting bits 20..30 gives e - 123 for a biased exponent
+            // e >= 123 and >= 1925 below (the borrow), whatever the sign, so
+            // |x| passes iff that field is < 1800 (e in [123, 1922]); q keeps
+            // its sign bit, which puts a negative q out of its window.  Integer
+            // VALU and two compares instead of seven fp64 compares and their
+            // mask arithmetic.
+            const unsigned hu = (unsigned)__double2hiint(cu), hv = (unsigned)__double2hiint(cv);
+            const unsigned hq = (unsigned)__double2hiint(q);
+            const unsigned eu = ((hu - (123u << 20)) >> 20) & 0x7FFu;
+            const unsigned ev = ((hv - (123u << 20)) >> 20) & 0x7FFu;
+            range_ok = (max(eu, ev) < 1800u) & (hq - (123u << 20) < (1800u << 20));
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

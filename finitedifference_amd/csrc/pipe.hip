@@ -873,7 +873,33 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
-        if (next) in = fetch(edge_tag, s + 1);
+        (void)next;
+    };
+
+    // One block: the LDS inputs are read two diagonals ahead (their latency
+    // hides behind a whole diagonal of arithmetic); everything a block reads
+    // was checked ready by block_missing.  Sweeps read one ahead, after the
+    // diagonal: a lane's trajectory switch (in diagonal s) decides which
+    // state and source table diagonal s + 1 reads.
+    auto run_block = [&](auto tag, const int sb) {
+        if constexpr (SWEEP) {
+            In a0 = fetch(tag, sb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                diagonal(tag, sb + u, false, a0);
+                if (u + 1 < U) a0 = fetch(tag, sb + u + 1);
+            }
+        } else {
+            In a0 = fetch(tag, sb), a1 = fetch(tag, sb + 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                In nx;
+                if (u + 2 < U) nx = fetch(tag, sb + u + 2);
+                diagonal(tag, sb + u, false, a0);
+                a0 = a1;
+                if (u + 2 < U) a1 = nx;
+            }
+        }
     };
 
     const int total = KW + kWave - 1;
@@ -936,19 +962,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const int sm_ = sb & (W - 1);
         const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
-            in = fetch(Edge(), sb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) diagonal(Edge(), sb + u, u + 1 < U, in);
+            run_block(Edge(), sb);
         } else if (nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
                    ct0 + U <= ncol_real) {
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
-            in = fetch(Steady(), sb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) diagonal(Steady(), sb + u, u + 1 < U, in);
+            run_block(Steady(), sb);
         } else {
-            in = fetch(Interior(), sb);
-#pragma unroll
-            for (int u = 0; u < U; ++u) diagonal(Interior(), sb + u, u + 1 < U, in);
+            run_block(Interior(), sb);
         }
     }
     if (lane == 0) {
