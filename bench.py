@@ -196,9 +196,10 @@ def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=2.4):
     if "interior_block" in d:
         # interior blocks of full strips run the steady variant when built
         inner = d.get("steady_block", d["interior_block"])
+        edge = d.get("steady_edge_block", d["edge_block"])
         fe = min(1.0, (64 / U + 1) / (W / U)) if W >= 128 else 1.0
-        cyc = (1 - fe) * inner["issue_cycles"] + fe * d["edge_block"]["issue_cycles"]
-        ins = (1 - fe) * inner["total"] + fe * d["edge_block"]["total"]
+        cyc = (1 - fe) * inner["issue_cycles"] + fe * edge["issue_cycles"]
+        ins = (1 - fe) * inner["total"] + fe * edge["total"]
     else:
         cyc, ins = d["block"]["issue_cycles"], d["block"]["total"]
     meas = avg_ms * 1e6 / diagonals * clock_ghz

@@ -145,7 +145,8 @@ struct MarchCell {
             const unsigned hq = (unsigned)__double2hiint(q);
             const unsigned eu = ((hu - (123u << 20)) >> 20) & 0x7FFu;
             const unsigned ev = ((hv - (123u << 20)) >> 20) & 0x7FFu;
-            range_ok = (max(eu, ev) < 1800u) & (hq - (123u << 20) < (1800u << 20));
+            const unsigned eq = (hq - (123u << 20)) >> 20;  // sign bit kept: negative q >= 2048
+            range_ok = max(max(eu, ev), eq) < 1800u;        // one v_max3 and one compare
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

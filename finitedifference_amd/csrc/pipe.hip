@@ -274,6 +274,7 @@ struct PipeLds {
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
+    v4u zeros[WIDE ? 8 : 1];  // wide: the south inflow of a boundary strip, read by block offsets
     v4u dump[WIDE ? kWave : 1];  // wide: write target of lanes with nothing to hand off (shared)
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
@@ -368,6 +369,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         sm.filled[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
+    if constexpr (WIDE)
+        if (threadIdx.x < 8) sm.zeros[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
     if constexpr (SWEEP) {
@@ -674,10 +677,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     typedef std::integral_constant<int, 0> Edge;
     typedef std::integral_constant<int, 1> Interior;
     typedef std::integral_constant<int, 2> Steady;
+    typedef std::integral_constant<int, 3> SteadyEdge;  // an edge block with the steady conditions
     unsigned noffs = 0;  // steady blocks: the top lane's north slot offset at the current diagonal
     auto fetch = [&](auto edge_tag, int s) -> In {
-        constexpr bool EDGE = decltype(edge_tag)::value == 0;
-        constexpr bool STEADY = decltype(edge_tag)::value == 2;
+        constexpr bool EDGE = decltype(edge_tag)::value == 0 || decltype(edge_tag)::value == 3;
+        constexpr bool STEADY = decltype(edge_tag)::value >= 2;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -701,6 +705,31 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
         else in.gw = v4u{0u, 0u, 0u, 0u};
         in.gs = lds_ld((has_south & (STEADY || s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
+        return in;
+    };
+
+    // Wide interior / steady blocks: no lane wraps a column inside the block,
+    // and the block starts at a multiple of U in the window (16) and south
+    // inbox (64) rings, so diagonal sb + u reads base + u -- the offsets fold
+    // into the LDS instructions' immediate fields.
+    struct Bases {
+        LDS v4u *wb, *cb, *ib;
+    };
+    auto bases_of = [&](int sb) -> Bases {
+        Bases b;
+        b.wb = &sm.win[k][sb % KWIN][lane];
+        b.cb = &sm.cc[k][(sb - lane) & (W - 1)];
+        b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : &sm.zeros[0];
+        return b;
+    };
+    auto fetch_b = [&](const Bases &b, int u) -> In {
+        In in;
+        in.nt = false;
+        in.src = 0.0;
+        in.xs = lds_ld(b.wb + u * kWave);
+        in.cs = b.cb[u];
+        in.gw = v4u{0u, 0u, 0u, 0u};
+        in.gs = lds_ld(b.ib + u);
         return in;
     };
 
@@ -750,8 +779,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // one diagonal (no waits: its block was checked); `next` = also read the
     // inputs of diagonal s + 1 (inside the block)
     auto diagonal = [&](auto edge_tag, const int s, const bool next, In &in) {
-        constexpr bool EDGE = decltype(edge_tag)::value == 0;
-        constexpr bool STEADY = decltype(edge_tag)::value == 2;
+        constexpr bool EDGE = decltype(edge_tag)::value == 0 || decltype(edge_tag)::value == 3;
+        constexpr bool STEADY = decltype(edge_tag)::value >= 2;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
@@ -854,9 +883,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // consumed inbound slots back to empty
         if constexpr (WIDE) {
             if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane], lempty);
-            if (has_south)
-                lds_st((need_s & (lane == 0)) ? &sm.ins[k][s & (kNI - 1)] : &sm.dump[lane],
-                       lempty);
+            // (the south slots are freed once per block, run_block)
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
             if (need_s && lane == 0) lds_st(&sm.ins[k][s & (kNI - 1)], lempty);
@@ -889,7 +916,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 diagonal(tag, sb + u, false, a0);
                 if (u + 1 < U) a0 = fetch(tag, sb + u + 1);
             }
-        } else {
+        } else if constexpr (!WIDE || decltype(tag)::value == 0 || decltype(tag)::value == 3) {
             In a0 = fetch(tag, sb), a1 = fetch(tag, sb + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -899,6 +926,24 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 a0 = a1;
                 if (u + 2 < U) a1 = nx;
             }
+        } else {
+            const Bases b = bases_of(sb);
+            In a0 = fetch_b(b, 0), a1 = fetch_b(b, 1);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                In nx;
+                if (u + 2 < U) nx = fetch_b(b, u + 2);
+                diagonal(tag, sb + u, false, a0);
+                a0 = a1;
+                if (u + 2 < U) a1 = nx;
+            }
+        }
+        if constexpr (WIDE) {
+            // the block's south inbox slots back to empty, one write: lane i
+            // frees diagonal sb + i's slot
+            if (has_south)
+                lds_st(((lane < U) & (sb + lane < KW)) ? &sm.ins[k][(sb + lane) & (kNI - 1)] : &sm.dump[lane],
+                       lempty);
         }
     };
 
@@ -907,7 +952,6 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
     // in flight -- into every diagonal.
     __builtin_amdgcn_s_waitcnt(0);
-    In in;
 #ifdef BURG_PIPE_PROF
     unsigned long long pf_vm = 0;
     const unsigned long long pf0 = __builtin_amdgcn_s_memtime();
@@ -961,11 +1005,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         const int sm_ = sb & (W - 1);
         const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
-        if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
-            run_block(Edge(), sb);
-        } else if (nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
-                   ct0 + U <= ncol_real) {
+        const bool steady = WIDE && nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
+                            ct0 + U <= ncol_real;
+        if (steady)
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
+        if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
+            // (narrow-or-equal tiles, W <= 64: one block's lanes span several
+            // steps, so the steady offsets do not hold -- plain edge blocks)
+            if (WIDE && W > kWave && steady) run_block(SteadyEdge(), sb);
+            else run_block(Edge(), sb);
+        } else if (steady) {
             run_block(Steady(), sb);
         } else {
             run_block(Interior(), sb);

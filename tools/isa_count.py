@@ -105,7 +105,8 @@ def main():
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
         names = {1: ["block"], 2: ["interior_block", "edge_block"],
-                 3: ["steady_block", "interior_block", "edge_block"]}[len(rr)]
+                 3: ["steady_block", "interior_block", "edge_block"],
+                 4: ["steady_block", "interior_block", "steady_edge_block", "edge_block"]}[len(rr)]
         res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}>"] = {
             "per_diagonal_averages": {nm: summarise(r) for nm, r in zip(names, rr)}}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
