@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -26,7 +26,7 @@ EXPORTS = (
     "burg_slab_connect", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
-    "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_lspg",
+    "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
     "burg_pod", "burg_pod_rsvd", "burg_run_npy",
 )
 KERNELS = {"residual": 0, "jvp": 1}
@@ -94,6 +94,14 @@ def load(path=None):
                 f"{p} is missing: build the HIP extension first "
                 "(python -c 'import __graft_entry__ as g; g.build()' or make -C "
                 "finitedifference_amd/csrc). There is no CPU fallback.")
+        # One HIP runtime per process: torch ships its own libamdhip64 under
+        # the same soname.  Loaded first, it is the runtime this library binds
+        # to; loaded after a HIP runtime is up, torch finds no GPU.  The
+        # decoder-ECSW variants (ecsw.py) and the benches use both.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lib = ctypes.CDLL(p)
         sig = {
             "burg_abi_version": (ctypes.c_int, []),
@@ -125,6 +133,10 @@ def load(path=None):
             "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
             "burg_ecsw_matrix": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int, _D, _D,
                                                 ctypes.POINTER(BurgStats)]),
+            "burg_ecsw_block_device": (ctypes.c_int, [_VP, ctypes.c_void_p, ctypes.c_void_p,
+                                                      ctypes.c_int, ctypes.c_void_p,
+                                                      ctypes.c_void_p,
+                                                      ctypes.POINTER(ctypes.c_float)]),
             "burg_lspg": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, _D, ctypes.c_int,
                                          ctypes.c_double, ctypes.c_double, _D, ctypes.c_int64,
                                          _D, ctypes.c_int64, _I32, _D, _D,

@@ -1612,6 +1612,42 @@ int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const doubl
     return rc;
 }
 
+// `p` must be device memory of the context's GPU (not host, not another GPU):
+// the ECSW block entry reads and writes through it from a kernel
+static int check_device_ptr(const burg_ctx *c, const void *p, const char *what)
+{
+    hipPointerAttribute_t at{};
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(BURG_EINVAL, "%s: not a HIP allocation", what);
+    }
+    if (at.type != hipMemoryTypeDevice || at.device != c->device)
+        return fail(BURG_EINVAL, "%s: not device memory of GPU %d", what, c->device);
+    return BURG_OK;
+}
+
+int burg_ecsw_block_device(burg_ctx *c, const double *d_state, const double *d_prev, int n_pod,
+                           const double *d_basis_t, double *d_C, float *kernel_ms)
+{
+    if (int e = check_ready(c)) return e;
+    if (kernel_ms) *kernel_ms = 0.f;
+    if (n_pod < 1) return fail(BURG_EINVAL, "n_pod must be >= 1");
+    if (!d_state || !d_prev || !d_basis_t || !d_C) return fail(BURG_EINVAL, "null array");
+    if (c->world > 1) return fail(BURG_EINVAL, "burg_ecsw_block_device: single-GPU contexts only");
+    if (int e = check_device_ptr(c, d_state, "state")) return e;
+    if (int e = check_device_ptr(c, d_prev, "prev_state")) return e;
+    if (int e = check_device_ptr(c, d_basis_t, "basis_t")) return e;
+    if (int e = check_device_ptr(c, d_C, "C")) return e;
+    HIPCHK(hipEventRecord(c->ev0, c->stream));
+    if (launch_ecsw(c->cf, d_state, d_prev, d_basis_t, n_pod, d_C, c->stream))
+        return fail(BURG_EHIP, "ecsw kernel launch failed");
+    HIPCHK(hipEventRecord(c->ev1, c->stream));
+    if (hipEventSynchronize(c->ev1) != hipSuccess)
+        return fail(BURG_EHIP, "ecsw: %s", hipGetErrorString(hipGetLastError()));
+    if (kernel_ms) (void)hipEventElapsedTime(kernel_ms, c->ev0, c->ev1);
+    return BURG_OK;
+}
+
 int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newton_max_its,
              double newton_rtol, double *snaps, int64_t ld_snaps, int snap_every,
              burg_stats *st, int32_t *step_iters, double *step_rel)

@@ -17,6 +17,11 @@ reference module ``hypernet2D`` for the FOM path (paths relative to
   param_to_snap_fn              C/hypernet2D.py:3081-3105
   get_saved_params              C/hypernet2D.py:3107-3109
   load_or_compute_snaps         C/hypernet2D.py:3111-3145
+  compute_ECSW_training_matrix_2D (+ _rnm, _rbf_nearest_neighbors,
+    _rbf_global, _gp)           C/hypernet2D.py:2719-3072 -> ecsw.py (HIP)
+  decode_/jac_rbf_nearest_neighbors, decode_/jac_rbf_global, decode_gp,
+    jac_gp, matern15_grad       C/hypernet2D.py:1279-1495, 1720-1808
+                                -> rom_decoders.py (host model code)
 
 The snapshot matrix is the reference's: float64, shape (2*nx*ny,
 num_steps + 1), C-contiguous, column j = state after j steps, u rows then v
@@ -34,6 +39,13 @@ from scipy.sparse.linalg import LinearOperator
 
 from .grid import fom_coefficients, make_2D_grid  # noqa: F401  (re-export)
 from .solver import DEFAULT_TOL, get_context
+from .ecsw import (compute_ECSW_training_matrix_2D_gp,  # noqa: F401  (re-export)
+                   compute_ECSW_training_matrix_2D_rbf_global,
+                   compute_ECSW_training_matrix_2D_rbf_nearest_neighbors,
+                   compute_ECSW_training_matrix_2D_rnm)
+from .rom_decoders import (decode_gp, decode_rbf_global,  # noqa: F401  (re-export)
+                           decode_rbf_nearest_neighbors, jac_gp, jac_rbf_global,
+                           jac_rbf_nearest_neighbors, matern15_grad)
 
 
 def make_ddx(grid_x):

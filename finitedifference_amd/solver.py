@@ -238,6 +238,30 @@ class FOMContext:
                                             _lib.dptr(basis), _lib.dptr(C), ctypes.byref(st)))
         return (C, st.as_dict()) if return_stats else C
 
+    def ecsw_block_device(self, state, prev, basis_t, out):
+        """One snapshot's ECSW block with its own basis, on device tensors
+        (burg_ecsw_block_device; the decoder variants of
+        compute_ECSW_training_matrix_2D, C/hypernet2D.py:2742-3072):
+        state, prev (2n,) and basis_t (npod, 2n) = V^T, float64 on this
+        context's GPU; out (npod, n) receives the block.  Returns the kernel
+        time in ms."""
+        import torch
+        dev = torch.device("cuda", self.device)
+        npod = basis_t.shape[0] if basis_t.dim() == 2 else -1
+        for name, t, shape in (("state", state, (self.m,)), ("prev", prev, (self.m,)),
+                               ("basis_t", basis_t, (npod, self.m)),
+                               ("out", out, (npod, self.m // 2))):
+            if t.dtype != torch.float64 or t.device != dev or not t.is_contiguous():
+                raise ValueError(f"{name} must be a contiguous float64 tensor on {dev}")
+            if tuple(t.shape) != shape:
+                raise ValueError(f"{name} has shape {tuple(t.shape)}, expected {shape}")
+        torch.cuda.current_stream(dev).synchronize()  # inputs written on torch's stream
+        ms = ctypes.c_float(0.0)
+        _lib.check(self._L.burg_ecsw_block_device(self._h, state.data_ptr(), prev.data_ptr(),
+                                                  int(npod), basis_t.data_ptr(), out.data_ptr(),
+                                                  ctypes.byref(ms)))
+        return ms.value
+
     def lspg(self, w0, num_steps, basis, max_its=20, relnorm_cutoff=1e-5, min_delta=0.1,
              keep_snaps=True, keep_coords=True):
         """LSPG PROM trajectory (burg_lspg; inviscid_burgers_implicit2D_LSPG,

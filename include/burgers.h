@@ -20,6 +20,10 @@
  *   burg_sweep          a loop of inviscid_burgers_implicit2D over a mu set
  *                       (C/run_prom.py:59-71, C/run_tests.py:38-49)
  *   burg_ecsw_matrix    C/hypernet2D.py:2719-2740 compute_ECSW_training_matrix_2D
+ *   burg_ecsw_block_device  one snapshot's C rows of the decoder variants
+ *                       C/hypernet2D.py:2742-3072 compute_ECSW_training_matrix_2D_rnm /
+ *                       _rbf_nearest_neighbors / _rbf_global / _gp (:2776-2781,
+ *                       :2840-2858, :2938-2956, :3050-3070), device pointers
  *   burg_lspg           C/hypernet2D.py:133-200   inviscid_burgers_implicit2D_LSPG
  *                       with C/hypernet2D.py:1859-1929 gauss_newton_LSPG
  *   burg_pod            C/hypernet2D.py:2670-2695   POD(method='svd') (np.linalg.svd)
@@ -31,7 +35,8 @@
  *   - State w has 2*nx*ny doubles: [u.ravel(), v.ravel()], u row-major
  *     (ny, nx), cell (r, c) at r*nx + c (C/run_fom.py:33-35).
  *   - All pointers passed in are HOST pointers owned by the caller and
- *     borrowed for the duration of the call; the library keeps none of them.
+ *     borrowed for the duration of the call; the library keeps none of them
+ *     (exception: burg_ecsw_block_device takes device pointers, checked).
  *   - Every function returns BURG_OK (0) or a negative BURG_E* code; the
  *     message of the last failure on the calling thread is burg_last_error().
  *   - One context per host thread; a context owns its device buffers,
@@ -46,7 +51,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 8
+#define BURG_ABI_VERSION 9
 
 enum burg_status {
     BURG_OK = 0,
@@ -250,6 +255,22 @@ int burg_run_npy(burg_ctx *ctx, const double *w0, int num_steps, int snap_every,
  * D2H time of C, steps = n_snaps.  Single-GPU contexts. */
 int burg_ecsw_matrix(burg_ctx *ctx, int n_snaps, const double *states, const double *prev_states,
                      int n_pod, const double *basis, double *C, burg_stats *stats);
+
+/* One snapshot's block of the ECSW training matrix with a per-snapshot
+ * basis: the decoder variants (compute_ECSW_training_matrix_2D_rnm,
+ * _rbf_nearest_neighbors, _rbf_global, _gp; C/hypernet2D.py:2742-3072)
+ * refit a reconstruction w(y) per snapshot and assemble C from
+ * R(w; prev) and J(w) V with V = dw/dy, a different basis per snapshot.
+ * All arrays are DEVICE memory of the context's GPU (the decoder's products
+ * live there; a host pointer is refused with BURG_EINVAL):
+ *   d_state, d_prev: 2n doubles; d_basis_t: (n_pod x 2n) C-order (V^T: the
+ *   columns of V contiguous); d_C: (n_pod x n) C-order output,
+ *   d_C[k*n + node] = R_u[node] (J V)_u[node,k] + R_v[node] (J V)_v[node,k].
+ * Stream-ordered on the context's stream and complete on return (callers
+ * producing the inputs on another stream synchronise it first).
+ * kernel_ms (may be NULL): the kernel's time.  Single-GPU contexts. */
+int burg_ecsw_block_device(burg_ctx *ctx, const double *d_state, const double *d_prev,
+                           int n_pod, const double *d_basis_t, double *d_C, float *kernel_ms);
 
 /* LSPG PROM time loop (inviscid_burgers_implicit2D_LSPG, C/hypernet2D.py:133-200,
  * with gauss_newton_LSPG, :1859-1929), with the context's problem (grid, dt,

@@ -27,6 +27,11 @@ Fixtures written
                      reference's own callbacks (res2D, exact_jac2D) on
                      reference snapshots, the driver's 3-step offset sampling
                      (C/run_HPROM_ecsw_joshua_.py:81-84) and a POD basis
+  ref_ecsw_variants.npz  the decoder variants compute_ECSW_training_matrix_2D_rnm /
+                     _rbf_nearest_neighbors / _rbf_global / _gp (:2742-3072) and
+                     their decoders (decode_* / jac_*, :1279-1808) on
+                     reference snapshots with fixed latent models
+                     (tests/ecsw_models.py)
   ref_lspg.npz       inviscid_burgers_implicit2D_LSPG (:133-200) + gauss_newton_LSPG
                      (:1859-1929) trajectories with POD bases of reference
                      snapshots at training mu, per-step Gauss-Newton counts
@@ -158,6 +163,83 @@ def make_ecsw(hn):
                     f"{tag}_meta": np.array([N, T, mu[0], mu[1], 0.05, npod, f])})
         print(f"ecsw {tag}: C {C.shape}")
     np.savez_compressed(os.path.join(HERE, "ref_ecsw.npz"), **out)
+
+
+RESID_RE = re.compile(r"^(Initial|Final)( reconstruction)? residual: ([0-9.eE+-]+)\s*$")
+
+
+def make_ecsw_variants(hn):
+    """ref_ecsw_variants.npz: the decoder variants of the ECSW training matrix
+    (C/hypernet2D.py:2742-3072) on reference snapshots at 16^2, with POD
+    primary/secondary bases of a 2-mu training set, a MinMaxScaler, a KD-tree,
+    global RBF weights per kernel, a fixed-hyper-parameter Matern(1.5) GP and
+    a float32 torch decoder for rnm (tests/ecsw_models.py rebuilds the same
+    objects from the stored arrays); plus the decoders' own outputs
+    (decode_* / jac_*, :1279-1808) at one reduced point, and the residuals
+    the variants print per snapshot."""
+    import torch
+    from scipy.spatial.distance import pdist, squareform
+    sys.path.insert(0, os.path.dirname(HERE))
+    import ecsw_models as em
+    from rbf_utils import RBFUtils  # reference module (build container only)
+    N, T, dt, rp, rs, eps, k = 16, 14, 0.05, 4, 8, 1.0, 6
+    mu = (4.56, 0.019)
+    gx, gy = hn.make_2D_grid(0, 100, 0, 100, N, N)
+    S = np.hstack([run_reference(hn, N, T, m)[0] for m in ((4.25, 0.015), (5.5, 0.03))])
+    snaps = run_reference(hn, N, T, mu)[0]
+    U = np.linalg.svd(S, full_matrices=False)[0]
+    basis, basis2 = U[:, :rp], U[:, rp:rp + rs]
+    qp_raw, Q = (basis.T @ S).T, (basis2.T @ S).T
+    scaler = em.scaler_of(qp_raw)
+    P = scaler.transform(qp_raw)
+    kdtree = em.kdtree_of(P)
+    s_use, s_prev = snaps[:, 3:T:3], snaps[:, 0:T - 3:3]
+    y_probe = basis.T @ s_use[:, 1]
+    res, jac = hn.inviscid_burgers_res2D, hn.inviscid_burgers_exact_jac2D
+    out = dict(meta=np.array([N, T, mu[0], mu[1], dt, rp, rs, eps, k]), snaps=snaps, basis=basis,
+               basis2=basis2, qp_raw=qp_raw, P=P, Q=Q, y_probe=y_probe)
+
+    def run(tag, fn, *args):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            C = fn(*args)
+        resid = [float(m.group(3)) for m in map(RESID_RE.match, buf.getvalue().splitlines()) if m]
+        assert len(resid) == 2 * s_use.shape[1], buf.getvalue()
+        out[f"{tag}_C"], out[f"{tag}_resid"] = C, np.array(resid)
+        print(f"ecsw variant {tag}: C {C.shape}, final residuals {resid[1::2]}")
+
+    phis = {"gaussian": RBFUtils.gaussian_rbf, "imq": RBFUtils.inverse_multiquadric_rbf,
+            "linear": RBFUtils.linear_rbf, "multiquadric": RBFUtils.multiquadric_rbf,
+            "matern": RBFUtils.matern_kernel}
+    for kt in em.RBF_KERNELS_NN:
+        run(f"nn_{kt}", hn.compute_ECSW_training_matrix_2D_rbf_nearest_neighbors, s_use, s_prev,
+            basis, basis2, eps, k, kdtree, P, Q, res, jac, gx, gy, dt, list(mu), scaler, kt)
+        out[f"nn_{kt}_dec"] = hn.decode_rbf_nearest_neighbors(y_probe, eps, k, kdtree, P, Q, basis,
+                                                              basis2, scaler, kt)
+        out[f"nn_{kt}_jac"] = hn.jac_rbf_nearest_neighbors(y_probe, kdtree, P, Q, basis, basis2,
+                                                           eps, k, scaler, kt)
+    for kt in em.RBF_KERNELS_GLOBAL:
+        W = np.linalg.solve(phis[kt](squareform(pdist(P)), eps) + 1e-8 * np.eye(P.shape[0]), Q)
+        out[f"glob_{kt}_W"] = W
+        run(f"glob_{kt}", hn.compute_ECSW_training_matrix_2D_rbf_global, s_use, s_prev, basis,
+            basis2, W, P, Q, res, jac, gx, gy, dt, list(mu), scaler, eps, kt)
+        out[f"glob_{kt}_dec"] = hn.decode_rbf_global(y_probe, W, P, basis, basis2, eps, scaler, kt)
+        out[f"glob_{kt}_jac"] = hn.jac_rbf_global(y_probe, W, P, Q, basis, basis2, eps, scaler, kt)
+    gp_par = np.array([1.5, 0.6, 1e-8])  # ConstantKernel value, Matern length scale, alpha
+    gp = em.gp_of(P, Q, *gp_par)
+    out["gp_par"] = gp_par
+    run("gp", hn.compute_ECSW_training_matrix_2D_gp, s_use, s_prev, basis, basis2, gp, res, jac,
+        gx, gy, dt, list(mu), scaler)
+    out["gp_dec"] = hn.decode_gp(y_probe, gp, basis, basis2, scaler)
+    out["gp_jac"] = hn.jac_gp(y_probe, gp, basis, basis2, scaler)
+    rng = np.random.default_rng(SEED)
+    A, b = 0.05 * rng.standard_normal((rs, rp)), 0.1 * rng.standard_normal(rs)
+    approx, jacfwd = em.nn_decoder_of(basis, basis2, A, b)
+    out["rnm_A"], out["rnm_b"] = A, b
+    run("rnm", hn.compute_ECSW_training_matrix_2D_rnm, s_use, s_prev, basis, approx, jacfwd, res,
+        jac, gx, gy, dt, list(mu))
+    assert torch.get_default_dtype() == torch.float32
+    np.savez_compressed(os.path.join(HERE, "ref_ecsw_variants.npz"), **out)
 
 
 GN_RE = re.compile(r"^iteration (\d+): relative norm ([0-9.eE+-]+)\s*$")
@@ -334,6 +416,8 @@ def main():
             make_ops(hn)
         if not only or "ecsw" in only:
             make_ecsw(hn)
+        if not only or "ecsw_variants" in only:
+            make_ecsw_variants(hn)
         if not only or "pod" in only:
             make_pod(hn)
         if not only or "lspg" in only:
