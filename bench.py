@@ -181,14 +181,19 @@ def end_to_end(nx=1024, T=500):
                     "matrix (burg_run_npy)"}
 
 
-def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=2.4):
+def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=None, clock_src=None):
     """Issue bound of the march kernel's compute waves: instructions per
     diagonal from the kernel's ISA (tools/isa_count.py -> profiles/r02/
     pipe_isa.json) at 4 cycles each (+12 per fp64 transcendental: one wave
     per SIMD issues at most one instruction per 4 cycles, tools/probes/
-    issue_probe.hip), against the measured time per diagonal at the nominal
-    2.4 GHz clock.  Wide tiles mix interior and edge blocks ((64/U + 1) of
+    issue_probe.hip), against the measured time per diagonal of the
+    wavefront (its T*W diagonals plus its fill, nx + rows: the last tile
+    starts that many diagonals after the first) at the kernel's effective
+    clock (GRBM_GUI_ACTIVE in profiles/pmc_traffic.json; the nominal 2.4 GHz
+    when absent).  Wide tiles mix interior and edge blocks ((64/U + 1) of
     every W/U blocks are edge blocks)."""
+    if clock_ghz is None:
+        clock_ghz, clock_src = 2.4, "nominal"
     try:
         d = json.load(open(isa_file))[kname]["per_diagonal_averages"]
     except Exception:
@@ -206,7 +211,7 @@ def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=2.4):
     return {"bound": "issue", "instructions_per_diagonal": round(ins, 1),
             "issue_cycles_per_diagonal": round(cyc, 1),
             "measured_cycles_per_diagonal": round(meas, 1), "frac": round(cyc / meas, 4),
-            "clock_ghz": clock_ghz, "diagonals_per_wave": diagonals,
+            "clock_ghz": clock_ghz, "clock_source": clock_src, "wavefront_diagonals": diagonals,
             "source": os.path.relpath(isa_file, ROOT)}
 
 
@@ -286,6 +291,15 @@ def read_pmc(path, key):
     if not e:
         return None, None
     return e.get("hbm_bytes_per_launch"), e.get("source")
+
+
+def read_clock(path, key):
+    """(effective clock GHz, source) of a kernel from profiles/pmc_traffic.json."""
+    try:
+        e = json.load(open(path)).get(key) or {}
+    except Exception:
+        return None, None
+    return e.get("effective_clock_ghz"), e.get("clock_source")
 
 
 def main():
@@ -418,8 +432,10 @@ def main():
             },
         }
         if st["engine"] == 2:
-            iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + 63, args.isa_file,
-                                 st["stream_w"], U=8 if st["stream_w"] > 16 else 4)
+            clk, csrc = read_clock(args.pmc_file, key)
+            iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + nx + rows,
+                                 args.isa_file, st["stream_w"], U=8 if st["stream_w"] > 16 else 4,
+                                 clock_ghz=clk, clock_src=csrc)
             if iss:
                 out["issue_roofline"] = iss
         if world == 1 and not args.no_1024:
@@ -463,8 +479,10 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
     gbs = BYTES_PER_CELL_UPDATE * upd / (ms * 1e-3) / 1e9
     traffic, tsrc = read_pmc(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
     kname = f"pipe_kernel<{st['stream_w']}, true>"
-    iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 63, isa_file, st["stream_w"],
-                         U=8 if st["stream_w"] > 16 else 4) if isa_file else None
+    clk, csrc = read_clock(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
+    iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 2 * nx, isa_file,
+                         st["stream_w"], U=8 if st["stream_w"] > 16 else 4, clock_ghz=clk,
+                         clock_src=csrc) if isa_file else None
     return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
             "issue_roofline": iss,
             "value": round(upd * steps / el / 1e6, 3), "unit": "Mcell-updates/s",

@@ -521,6 +521,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 break;
             }
             if (!__any(prog)) __builtin_amdgcn_s_sleep(2);
+#ifdef BURG_COMM_SLEEP
+            else __builtin_amdgcn_s_sleep(BURG_COMM_SLEEP);
+#endif
             if (lds_ldi(&sm.perm[5])) break;
         }
         if (lane == 0) atomicAdd(&a.stats->why[5], iters);

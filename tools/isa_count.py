@@ -23,7 +23,8 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "finitedifference_amd", "csrc", "pipe.hip")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
-         "-Wno-bitwise-instead-of-logical"]
+         "-Wno-bitwise-instead-of-logical",
+         "-mllvm", "-amdgpu-sched-strategy=max-ilp"]  # as the Makefile builds pipe.hip
 
 
 def kind(op):
