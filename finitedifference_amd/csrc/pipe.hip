@@ -269,7 +269,8 @@ struct PipeLds {
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
-    v4u cc[4][W];           // per wave: {hx, src} of the tile's columns
+    v4u cc[4][W + (WIDE ? 8 : 0)];  // per wave: {hx, src} of the tile's columns (wide: + the
+                                    // first 8 again, so a block's lane reads base + u unwrapped)
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
@@ -388,8 +389,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
-        for (int c = lane; c < W; c += kWave) {
-            const d2 v = a.colc[(size_t)(tj0 + wave) * W + c];
+        for (int c = lane; c < W + (WIDE ? 8 : 0); c += kWave) {
+            const d2 v = a.colc[(size_t)(tj0 + wave) * W + (c & (W - 1))];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
         if constexpr (!WIDE) {
@@ -680,10 +681,18 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     typedef std::integral_constant<int, 0> Edge;
     typedef std::integral_constant<int, 1> Interior;
     typedef std::integral_constant<int, 2> Steady;
-    typedef std::integral_constant<int, 3> SteadyEdge;  // an edge block with the steady conditions
+    // SteadyEdge: a wide-tile edge block (W > 64) with the steady conditions:
+    // each lane meets column 0 and column W-1 at most once in the block, at
+    // block-constant diagonals (uw, ue) and steps -- its west granule is read
+    // once, its hand-off addresses are fixed, the inputs come by block base
+    typedef std::integral_constant<int, 3> SteadyEdge;
+    int se_uw = U, se_ue = U;  // SteadyEdge: the lane's column-0 / column-(W-1) diagonal in the block
+    v4u se_gw = v4u{0u, 0u, 0u, 0u};
+    LDS v4u *se_eaddr = nullptr;
+    unsigned se_eoff = kOOB;
     unsigned noffs = 0;  // steady blocks: the top lane's north slot offset at the current diagonal
     auto fetch = [&](auto edge_tag, int s) -> In {
-        constexpr bool EDGE = decltype(edge_tag)::value == 0 || decltype(edge_tag)::value == 3;
+        constexpr bool EDGE = decltype(edge_tag)::value == 0;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
         const int t = s - lane;
         const int c = t & (W - 1);
@@ -779,16 +788,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         return why;
     };
 
-    // one diagonal (no waits: its block was checked); `next` = also read the
-    // inputs of diagonal s + 1 (inside the block)
-    auto diagonal = [&](auto edge_tag, const int s, const bool next, In &in) {
-        constexpr bool EDGE = decltype(edge_tag)::value == 0 || decltype(edge_tag)::value == 3;
+    // one diagonal, diagonal u of its block (no waits: the block was checked)
+    auto diagonal = [&](auto edge_tag, const int s, const int u, In &in) {
+        constexpr bool EDGE = decltype(edge_tag)::value == 0;
+        constexpr bool SE = decltype(edge_tag)::value == 3;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
         const int t = s - lane;
         const int c = t & (W - 1);
         const int q = t >> LW;
         const bool valid = STEADY || (unsigned)t < (unsigned)KW;
-        const bool at0 = EDGE & (c == 0), atE = EDGE & (c == W - 1);
+        const bool at0 = SE ? u == se_uw : EDGE & (c == 0);
+        const bool atE = SE ? u == se_ue : EDGE & (c == W - 1);
         const bool need_w = has_west & at0 & valid & rowok;
         const bool need_s = has_south & (STEADY || s < KW);  // wave-uniform (lane 0 consumes)
         const bool out_e = atE & valid & rowok;
@@ -815,7 +825,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const MarchCell::Row rw{ay, hy, lbu};
         // ---- the cell's chain
         if (at0) {
-            const d2 gv = as_d2(in.gw);
+            const d2 gv = as_d2(SE ? se_gw : in.gw);
             e0 = gv.x;
             e1 = gv.y;
         }
@@ -857,7 +867,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const int aq = a.qbase + q;
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
-        if constexpr (WIDE) {
+        if constexpr (SE) {
+            lds_st(atE ? se_eaddr : &sm.dump[lane], eo);
+        } else if constexpr (WIDE) {
             if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane], eo);
         } else {
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
@@ -865,7 +877,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // wide tiles issue every store on every diagonal (out-of-range offsets
         // are dropped): exactly 3 per edge and 2 per interior diagonal, which
         // the vmcnt of done[] counts
-        if (EDGE && (WIDE || east_glob))
+        if constexpr (SE)
+            st_dev(wbox, atE ? se_eoff : kOOB, eo);
+        else if (EDGE && (WIDE || east_glob))
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
         if (WIDE || has_north) {
             // one store flavour for both targets: sc0 sc1 (system scope) reaches
@@ -903,7 +917,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 src_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
             }
         }
-        (void)next;
+        (void)u;
     };
 
     // One block: the LDS inputs are read two diagonals ahead (their latency
@@ -916,30 +930,48 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             In a0 = fetch(tag, sb);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                diagonal(tag, sb + u, false, a0);
+                diagonal(tag, sb + u, u, a0);
                 if (u + 1 < U) a0 = fetch(tag, sb + u + 1);
             }
-        } else if constexpr (!WIDE || decltype(tag)::value == 0 || decltype(tag)::value == 3) {
+        } else if constexpr (!WIDE || decltype(tag)::value == 0) {
             In a0 = fetch(tag, sb), a1 = fetch(tag, sb + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 In nx;
                 if (u + 2 < U) nx = fetch(tag, sb + u + 2);
-                diagonal(tag, sb + u, false, a0);
+                diagonal(tag, sb + u, u, a0);
                 a0 = a1;
                 if (u + 2 < U) a1 = nx;
             }
         } else {
+            int se_qw = 0;
+            bool se_in = false;
+            if constexpr (decltype(tag)::value == 3) {
+                // the lane's column-0 and column-(W-1) cells in this block
+                const int c0 = (sb - lane) & (W - 1);
+                se_uw = (W - c0) & (W - 1);
+                se_ue = (W - 1 - c0) & (W - 1);
+                se_qw = (sb + se_uw - lane) >> LW;
+                const int qe = (sb + se_ue - lane) >> LW;
+                se_in = has_west & (se_uw < U);
+                const bool oute = se_ue < U;
+                se_gw = lds_ld(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.zero);
+                se_eaddr = (east_lds & oute) ? &sm.ewe[k][qe & (kRL - 1)][lane] : &sm.dump[lane];
+                se_eoff = (east_glob & oute) ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
+            }
             const Bases b = bases_of(sb);
             In a0 = fetch_b(b, 0), a1 = fetch_b(b, 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 In nx;
                 if (u + 2 < U) nx = fetch_b(b, u + 2);
-                diagonal(tag, sb + u, false, a0);
+                diagonal(tag, sb + u, u, a0);
                 a0 = a1;
                 if (u + 2 < U) a1 = nx;
             }
+            // SteadyEdge: the west granule consumed in this block back to empty
+            if (decltype(tag)::value == 3 && has_west)
+                lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane], lempty);
         }
         if constexpr (WIDE) {
             // the block's south inbox slots back to empty, one write: lane i
