@@ -619,6 +619,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const int tj = tj0 + k;
     const int tile = ti * ntj + tj;
     const bool rowok = lane < nrow;
+    const unsigned long long rowmask = __builtin_amdgcn_ballot_w64(rowok);
     const bool has_west = tj > 0;
     const bool has_south = south_dev || south_host;
     const bool east_lds = k < 3 && k + 1 < nval;
@@ -835,7 +836,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         double oe0, oe1, on0, on1, o0, o1;
         bool ok;
         MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
-        if (__builtin_expect(any_lane(!ok & valid & rowok), 0)) {
+        // (ballots of the single compares, combined on the scalar unit: a
+        // ballot of the combined lane predicate costs a select and a compare)
+        const unsigned long long bad =
+            __builtin_amdgcn_ballot_w64(!ok) &
+            (STEADY ? rowmask : __builtin_amdgcn_ballot_w64(valid) & rowmask);
+        if (__builtin_expect(bad != 0, 0)) {
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             ++ieee_n;
             // the only place a non-finite state can appear (the fast path's
