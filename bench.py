@@ -376,6 +376,9 @@ def main():
         hin, hout = ctx.halo_modes()
         halo = {0: None, 1: "pinned host memory", 2: "consumer GPU memory over IPC (xGMI)"}[
             hout if rank == 0 else hin]
+        note = ctx.halo_note()
+        if note:
+            halo += f" ({note})"
     ctx.close()  # give the trajectory ring back before the secondary probes
     if rank == 0:
         st = st_main

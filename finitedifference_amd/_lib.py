@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -23,7 +23,7 @@ ENGINES = {"stream": 0, "tiles": 1, "pipe": 2}
 # Every symbol include/burgers.h declares (checked by tests/test_capi.py).
 EXPORTS = (
     "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_ctx_create_slab",
-    "burg_slab_connect", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
+    "burg_slab_connect", "burg_slab_verify", "burg_slab_halo_note", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
@@ -111,6 +111,8 @@ def load(path=None):
             "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.c_char_p,
                                                                          ctypes.POINTER(_VP)]),
             "burg_slab_connect": (ctypes.c_int, [_VP]),
+            "burg_slab_verify": (ctypes.c_int, [_VP]),
+            "burg_slab_halo_note": (ctypes.c_char_p, [_VP]),
             "burg_slab_halo_mode": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int),
                                                    ctypes.POINTER(ctypes.c_int)]),
             "burg_ctx_destroy": (None, [_VP]),

@@ -180,6 +180,10 @@ bool pipe_sweep_width_supported(int W);
 int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);
+// halo ring self-test: system-scope store of `put` at granule put_at (>= 0),
+// then poll granule get_at (>= 0) for `want` up to `seconds`; got = last read
+int halo_probe(void *ring, size_t bytes, int put_at, const unsigned put[4], int get_at,
+               const unsigned want[4], double seconds, unsigned got[4], hipStream_t st);
 int launch_basis_transpose(const double *b, double *bt, size_t m, int npod, hipStream_t st);
 int launch_ecsw(const Coeffs &cf, const double *w, const double *wp, const double *bt, int npod,
                 double *cblk, hipStream_t st);

@@ -146,6 +146,8 @@ struct burg_ctx {
     int halo_in_mode = 0, halo_out_mode = 0;             // 0 unknown, 1 host, 2 device
     size_t halo_bytes = 0;
     bool halo_connected = false;
+    bool halo_out_resolved = false;  // producer: took the consumer's verdict (first launch)
+    std::string halo_note;           // why a device ring was not used
 
     size_t m() const { return 2 * (size_t)nx * nrows; }
     size_t n() const { return (size_t)nx * nrows; }
@@ -317,6 +319,7 @@ int read_stats(burg_ctx *c, burg_stats *st)
 }
 
 int halo_resolve_in(burg_ctx *c);  // multi-GPU halo rings (below)
+void halo_resolve_out(burg_ctx *c);
 
 // ---- streaming engine -------------------------------------------------------
 void stream_free(burg_ctx *c)
@@ -437,7 +440,10 @@ int stream_setup(burg_ctx *c)
     }
     if (c->world > 1 && !c->halo_connected)
         return fail(BURG_ESTATE, "slab context not connected (burg_slab_connect) to its neighbours");
-    if (c->world > 1) CHK(halo_resolve_in(c));
+    if (c->world > 1) {
+        CHK(halo_resolve_in(c));
+        halo_resolve_out(c);
+    }
     if (!c->colc_ready) {
         CHK(launch_colc(c->cf, c->sp.ntj * c->sp.W, c->d_colc, c->stream));
         c->colc_ready = true;
@@ -857,10 +863,19 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
 struct HaloCtl {
     uint32_t magic;
     uint32_t dev_ok;  // consumer: device ring exported
-    volatile uint32_t choice;  // producer: 1 host ring, 2 device ring
+    volatile uint32_t choice;  // producer: 1 host ring, 2 device ring (the consumer may
+                               // demote 2 to 1 in burg_slab_verify)
     uint32_t pad;
     hipIpcMemHandle_t handle;
 };
+// Device-ring self-test: two granules just past the ring (never part of the
+// step slots).  The consumer stores kProbeC at granule 1 when it exports the
+// ring; the producer, having opened it, must read kProbeC back over xGMI and
+// stores kProbeP at granule 0, which the consumer must read in
+// burg_slab_verify.  Either check failing puts the boundary on the host ring.
+constexpr size_t kHaloProbeBytes = 256;
+constexpr unsigned kProbeC[4] = {0xB0A6C7A1u, 0x3FF0C0DEu, 0x12345678u, 0x40090000u};
+constexpr unsigned kProbeP[4] = {0x5A5A0001u, 0x3FF1C0DEu, 0x9ABCDEF0u, 0x400A0000u};
 constexpr uint32_t kHaloMagic = 0xB0A6C7A1u;
 constexpr size_t kHaloCtlBytes = 4096;
 static_assert(sizeof(HaloCtl) <= kHaloCtlBytes, "halo control page");
@@ -934,15 +949,21 @@ void halo_export_device_ring(burg_ctx *c, HaloCtl *ctl)
 {
     if (halo_force_host()) return;
     void *r = nullptr;
-    if (hipExtMallocWithFlags(&r, c->halo_bytes, hipDeviceMallocUncached) != hipSuccess || !r) {
+    const size_t bytes = c->halo_bytes + kHaloProbeBytes;
+    if (hipExtMallocWithFlags(&r, bytes, hipDeviceMallocUncached) != hipSuccess || !r) {
         (void)hipGetLastError();
+        c->halo_note = "hipExtMallocWithFlags(uncached) failed";
         return;
     }
     hipIpcMemHandle_t h{};
-    if (launch_pipe_fill(r, c->halo_bytes / 16, 0, c->stream) != 0 ||
+    const int probe0 = (int)(c->halo_bytes / 16);
+    unsigned got[4];
+    if (launch_pipe_fill(r, bytes / 16, 0, c->stream) != 0 ||
+        halo_probe(r, bytes, probe0 + 1, kProbeC, -1, kProbeC, 0.0, got, c->stream) != 0 ||
         hipStreamSynchronize(c->stream) != hipSuccess || hipIpcGetMemHandle(&h, r) != hipSuccess) {
         (void)hipGetLastError();
         (void)hipFree(r);
+        c->halo_note = "device ring export failed";
         return;
     }
     c->halo_in_ring = (d2 *)r;
@@ -970,9 +991,55 @@ int halo_resolve_in(burg_ctx *c)
     return 0;
 }
 
+// producer, first launch (after the barrier that follows burg_slab_verify):
+// take the consumer's verdict on the device ring
+void halo_resolve_out(burg_ctx *c)
+{
+    if (c->halo_out_resolved || c->rank + 1 >= c->world) return;
+    c->halo_out_resolved = true;
+    HaloCtl *ctl = halo_ctl(c, c->halo_out_host);
+    if (c->halo_out_mode == 2 && __atomic_load_n(&ctl->choice, __ATOMIC_ACQUIRE) == 1) {
+        c->halo_out_dev = c->halo_out_hostdev;
+        c->halo_out_mode = 1;
+        c->halo_note = "the rank above rejected the device ring (burg_slab_verify)";
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int burg_slab_verify(burg_ctx *c)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (c->world == 1 || c->rank == 0) return BURG_OK;
+    if (!c->halo_connected)
+        return fail(BURG_ESTATE, "burg_slab_verify before burg_slab_connect");
+    HIPCHK(hipSetDevice(c->device));
+    HaloCtl *ctl = halo_ctl(c, c->halo_in_host);
+    const uint32_t ch = __atomic_load_n(&ctl->choice, __ATOMIC_ACQUIRE);
+    if (ch == 0)
+        return fail(BURG_ESTATE, "rank %d: the rank below has not connected to the halo ring yet",
+                    c->rank);
+    if (ch != 2 || !c->halo_in_ring) return BURG_OK;
+    const size_t bytes = c->halo_bytes + kHaloProbeBytes;
+    unsigned got[4] = {0, 0, 0, 0};
+    const int pr = halo_probe(c->halo_in_ring, bytes, -1, kProbeP, (int)(c->halo_bytes / 16),
+                              kProbeP, 0.25, got, c->stream);
+    // BURG_HALO_REJECT=1: test hook, reject a good ring (exercises the demotion)
+    const char *rej = std::getenv("BURG_HALO_REJECT");
+    const bool force = rej && std::strcmp(rej, "1") == 0;
+    if (force || pr != 0 || std::memcmp(got, kProbeP, sizeof got) != 0) {
+        (void)hipGetLastError();
+        c->halo_note = force ? "device ring rejected by BURG_HALO_REJECT"
+                       : pr  ? "consumer probe kernel failed"
+                             : "the producer's probe store never arrived in the device ring";
+        __atomic_store_n(&ctl->choice, 1u, __ATOMIC_RELEASE);  // both sides use the host ring
+    }
+    return BURG_OK;
+}
+
+const char *burg_slab_halo_note(burg_ctx *c) { return c ? c->halo_note.c_str() : ""; }
 
 int burg_abi_version(void) { return BURG_ABI_VERSION; }
 
@@ -1083,11 +1150,25 @@ int burg_slab_connect(burg_ctx *c)
         if (ctl->dev_ok && !halo_force_host()) {
             void *p = nullptr;
             if (hipIpcOpenMemHandle(&p, ctl->handle, hipIpcMemLazyEnablePeerAccess) == hipSuccess && p) {
-                c->halo_out_ipc = p;
-                c->halo_out_dev = (d2 *)p;
-                choice = 2;
+                // read the consumer's probe back and leave ours, across the link
+                const size_t bytes = c->halo_bytes + kHaloProbeBytes;
+                const int probe0 = (int)(c->halo_bytes / 16);
+                unsigned got[4] = {0, 0, 0, 0};
+                const int pr = halo_probe(p, bytes, probe0, kProbeP, probe0 + 1, kProbeC, 0.25, got,
+                                          c->stream);
+                if (pr == 0 && std::memcmp(got, kProbeC, sizeof got) == 0) {
+                    c->halo_out_ipc = p;
+                    c->halo_out_dev = (d2 *)p;
+                    choice = 2;
+                } else {
+                    (void)hipGetLastError();
+                    (void)hipIpcCloseMemHandle(p);
+                    c->halo_note = pr ? "producer probe kernel failed"
+                                      : "producer read a wrong probe from the device ring";
+                }
             } else {
                 (void)hipGetLastError();  // fall back to the host ring
+                c->halo_note = "hipIpcOpenMemHandle failed";
             }
         }
         c->halo_out_mode = (int)choice;

@@ -1085,6 +1085,30 @@ __global__ void pipe_fill_kernel(v4u *p, size_t n, int color)
     if (i < n) p[i] = sent_g(color);
 }
 
+// Halo ring self-test (one lane): store `put` at granule put_at (if >= 0) and
+// poll granule get_at (if >= 0) for `want` for at most `ticks` of the 100 MHz
+// realtime clock, both at system scope as the pipe kernel's halo accesses;
+// out = the last value read.
+__global__ void halo_probe_kernel(v4u *ring, unsigned bytes, int put_at, v4u put, int get_at,
+                                  v4u want, long long ticks, v4u *out)
+{
+    if (threadIdx.x != 0) return;
+    const __amdgpu_buffer_rsrc_t rs = rsrc(ring, bytes);
+    if (put_at >= 0) st_sys(rs, (unsigned)put_at * 16u, put);
+    v4u g = want;
+    if (get_at >= 0) {
+        const long long t0 = now_rt();
+        for (;;) {
+            g = ld_sys(rs, (unsigned)get_at * 16u);
+            if ((g.x == want.x && g.y == want.y && g.z == want.z && g.w == want.w) ||
+                now_rt() - t0 > ticks)
+                break;
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    *out = g;
+}
+
 template <bool SWEEP>
 const void *kernel_of(int W)
 {
@@ -1197,6 +1221,29 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     const int threads = W > 16 ? 6 * kWave : 5 * kWave;
     if (hipLaunchKernel(fn, dim3(blocks), dim3(threads), kargs, dyn, st) != hipSuccess) return -3;
     return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+int halo_probe(void *ring, size_t bytes, int put_at, const unsigned put[4], int get_at,
+               const unsigned want[4], double seconds, unsigned got[4], hipStream_t st)
+{
+    if (bytes < 16 || bytes > 0xFFFFFFF0u) return -1;
+    v4u *d_out = nullptr;
+    if (hipMalloc(&d_out, sizeof(v4u)) != hipSuccess) return -3;
+    const v4u p = {put[0], put[1], put[2], put[3]};
+    const v4u w = {want[0], want[1], want[2], want[3]};
+    hipLaunchKernelGGL(halo_probe_kernel, dim3(1), dim3(kWave), 0, st, (v4u *)ring, (unsigned)bytes,
+                       put_at, p, get_at, w, (long long)(seconds * 1e8), d_out);
+    v4u h{};
+    const bool ok = hipGetLastError() == hipSuccess &&
+                    hipMemcpyAsync(&h, d_out, sizeof(v4u), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                    hipStreamSynchronize(st) == hipSuccess;
+    (void)hipFree(d_out);
+    if (!ok) return -3;
+    got[0] = h.x;
+    got[1] = h.y;
+    got[2] = h.z;
+    got[3] = h.w;
+    return 0;
 }
 
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st)

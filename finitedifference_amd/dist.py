@@ -7,10 +7,12 @@ y = 0).  The upwind march couples a slab only to the row just below it
 (C/hypernet2D.py:2410-2416: backward differences), so the exchange is
 one-way, rank k -> k+1: the north outflow of rank k's top row is the south
 inflow of rank k+1's bottom row.  Inside libburgers_hip that stream runs
-GPU-to-GPU through a ring in shared pinned host memory while both time loops
-are running; this module only agrees on the ring's
-name, orders context creation around a barrier, and splits / assembles
-states and snapshot matrices in the reference layout.
+GPU-to-GPU while both time loops are running, through a ring in the
+consumer GPU's memory (producer stores over xGMI) or, as the fallback, in
+shared pinned host memory; this module only agrees on
+the ring's name, orders context creation, connection and the ring self-test
+around barriers, and splits / assembles states and snapshot matrices in the
+reference layout.
 """
 import os
 import secrets
@@ -71,7 +73,9 @@ def agree_halo_name(dist=None):
 def make_slab_context(nx, ny, rank=0, world=1, device=0, dist=None, halo_name=None, **opts):
     """Context for rank `rank`'s slab.  world > 1: every rank must call this
     together (it creates this rank's inbound halo ring, waits on a barrier
-    until all rings exist, then attaches the outbound one)."""
+    until all rings exist, attaches the outbound one, and after a second
+    barrier checks that the neighbour's probe store crossed the link into a
+    device ring -- a failed check moves that boundary to the host ring)."""
     if world == 1:
         return FOMContext(nx, ny, device, **opts)
     if dist is None:
@@ -82,5 +86,7 @@ def make_slab_context(nx, ny, rank=0, world=1, device=0, dist=None, halo_name=No
     ctx = FOMContext.slab(nx, ny, row0, rows, rank, world, halo_name, device, **opts)
     dist.barrier()
     ctx.connect()
+    dist.barrier()
+    ctx.verify()
     dist.barrier()
     return ctx

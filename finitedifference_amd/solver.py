@@ -47,6 +47,16 @@ class FOMContext:
     def connect(self):
         _lib.check(self._L.burg_slab_connect(self._h))
 
+    def verify(self):
+        """Consumer-side self-test of a device halo ring (after a barrier that
+        follows every rank's connect(); a barrier must follow it before the
+        first launch).  A failed test moves the boundary to the host ring."""
+        _lib.check(self._L.burg_slab_verify(self._h))
+
+    def halo_note(self):
+        """Why this slab's halo is not on a device ring ('' if it is)."""
+        return (self._L.burg_slab_halo_note(self._h) or b"").decode()
+
     def halo_modes(self):
         """(in, out) halo ring placement of a slab context: 0 none (end rank),
         1 pinned host memory, 2 the consumer GPU's device memory (IPC).  The

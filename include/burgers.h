@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 9
+#define BURG_ABI_VERSION 10
 
 enum burg_status {
     BURG_OK = 0,
@@ -131,11 +131,23 @@ int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);
  * same job-unique string on every rank, 1-64 chars).  This call creates the
  * ring this rank consumes; after EVERY rank has created its context (a host
  * barrier), call burg_slab_connect to attach the ring this rank produces
- * into, and run a second barrier before the first launch.  world == 1
- * behaves as burg_ctx_create. */
+ * into, then (second barrier) burg_slab_verify, and run a third barrier
+ * before the first launch.  world == 1 behaves as burg_ctx_create. */
 int burg_ctx_create_slab(int device, int nx, int ny_total, int row0, int nrows,
                          int rank, int world, const char *halo_name, burg_ctx **out);
 int burg_slab_connect(burg_ctx *ctx);
+/* Consumer-side check of a device-memory halo ring (no-op on rank 0 and on
+ * host rings): the producer's probe store, made over the link in
+ * burg_slab_connect, must have arrived; if not, the boundary moves to the
+ * pinned host ring on both sides (the producer adopts that at its first
+ * launch, so a barrier must separate this call from any launch).  The
+ * producer's own check (it reads the consumer's probe back) runs inside
+ * burg_slab_connect.  Replaces nothing in the reference (its FOM is one
+ * process); it guards the rows-slab halo of SURVEY.md section 8(e). */
+int burg_slab_verify(burg_ctx *ctx);
+/* Why a slab context's halo is not on a device ring ("" when it is, or for
+ * world == 1); valid until the next call on the context. */
+const char *burg_slab_halo_note(burg_ctx *ctx);
 /* Where the halo rings live: *in_mode for the ring this rank consumes,
  * *out_mode for the one it produces into: 0 none (end rank), 1 pinned host
  * memory, 2 the consumer GPU's device memory (IPC). */

@@ -344,14 +344,16 @@ def _halo_modes(tmp_path, world):
 
 
 @pytest.mark.parametrize("N,world,T,halo", [(128, 2, 9, "device"), (150, 3, 7, "device"),
-                                            (150, 3, 7, "host")])
+                                            (150, 3, 7, "host"), (150, 3, 7, "reject")])
 def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T, halo):
     """Multi-GPU path, rehearsed on one GPU: `world` processes, one slab each,
     all on device 0, exchanging the halo while their time loops run
     concurrently -- through each consumer's device-memory ring opened over IPC
-    (the default), or the pinned host rings (BURG_HALO=host).  The assembled
-    trajectory is the single-grid sequential march bit for bit."""
-    env = {} if halo == "device" else {"BURG_HALO": "host"}
+    (the default), or the pinned host rings (BURG_HALO=host; "reject": the
+    device rings pass the producer's probe but every consumer's
+    burg_slab_verify rejects them, so both sides must move to the host ring).
+    The assembled trajectory is the single-grid sequential march bit for bit."""
+    env = {"device": {}, "host": {"BURG_HALO": "host"}, "reject": {"BURG_HALO_REJECT": "1"}}[halo]
     _run_slabs(tmp_path, N, T, world, **env)
     mode = 2 if halo == "device" else 1
     want = [(0 if r == 0 else mode, 0 if r == world - 1 else mode) for r in range(world)]
