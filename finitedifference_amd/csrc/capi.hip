@@ -119,6 +119,7 @@ struct burg_ctx {
     bool sp_ready = false, colc_ready = false;
     d2 *d_colc = nullptr, *d_boxes = nullptr, *d_ring = nullptr;
     size_t box16 = 0, ring_entries = 0;
+    bool ring_maxed = false;  // the ring was sized to the free-memory limit
     unsigned *d_err = nullptr;
     StreamStats *d_sstats = nullptr;
     // pipe engine (pipe.hip): effective engine of march runs, workgroups per
@@ -680,18 +681,23 @@ int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats 
     const int W = c->sp.W;
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     long long C = std::min(num_steps, stream_max_steps(c));
-    if ((size_t)(C * W + W + 96) * per_entry > c->ring_entries * sizeof(d2)) {
+    const long long have_L = (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave));
+    // a ring already sized to the memory limit is reused as it is: the next
+    // call would only get the same size back, after a free and a fresh
+    // allocation of up to ~240 GB (seconds per call at 8192^2)
+    if (C * W + W + 96 > have_L && !(c->ring_maxed && have_L >= 2 * W + 96)) {
         // need a (bigger) ring: size it against free memory
         dfree(c->d_ring);
         c->ring_entries = 0;
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
         const long long Lmax = (long long)(freeb / 100 * 85 / per_entry);
-        C = std::min<long long>(C, (Lmax - W - 96) / W);
+        const long long Cmem = (Lmax - W - 96) / W;
+        c->ring_maxed = Cmem < C;
+        C = std::min<long long>(C, Cmem);
         if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
     } else {
-        C = std::min<long long>(C, ((long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave)) -
-                                    W - 96) / W);
+        C = std::min<long long>(C, (have_L - W - 96) / W);
     }
     const long long L = C * W + W + 96;
     if (int e = ensure_ring(c, L)) return e;
@@ -747,9 +753,11 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
     }
     if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
     const long long L = C * W + W + 96;
-    dfree(c->d_ring);
-    c->ring_entries = 0;
-    if (int e = ensure_ring(c, L)) return e;
+    if ((size_t)c->sp.ntiles * (size_t)L * kWave > c->ring_entries) {  // else reuse the ring
+        dfree(c->d_ring);
+        c->ring_entries = 0;
+        if (int e = ensure_ring(c, L)) return e;
+    }
 
     // snapshot staging: S columns at a time
     int S = 0;
