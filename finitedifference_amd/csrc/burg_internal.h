@@ -198,6 +198,7 @@ struct LspgArgs {
     const double *btT;   // basis, (npod, 2n), each plane transposed
     const double *r;     // residual R(w; wp) (2n)
     int npod;
+    const double *bk;    // basis blocked by 32-cell tiles (lspg_gram_blocked): [tile][k][4][32]
 };
 int lspg_cols(int npod);
 size_t lspg_partial_count(int nx, int npod);
@@ -206,6 +207,12 @@ int launch_lspg_expand(const double *bt, const double *y, int npod, size_t m, do
 int launch_lspg_project(const double *bt, const double *x, int npod, size_t m, double *scratch,
                         double *y, hipStream_t st);
 int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t st);
+// the Gram kernel for npod reads the blocked basis (LspgArgs::bk): its size in
+// doubles, and the kernel that builds it from bt / btT
+bool lspg_gram_blocked(int npod);
+size_t lspg_blocked_count(size_t n, int npod);
+int launch_lspg_block_basis(const double *bt, const double *btT, size_t n, int npod, double *bk,
+                            hipStream_t st);
 int launch_lspg_solve(const double *G, int npod, double *y, double *dy, unsigned *err,
                       hipStream_t st);
 // the same with rocSOLVER potrf/potrs (handle: a rocblas_handle on st)

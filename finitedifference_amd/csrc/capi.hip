@@ -2108,7 +2108,8 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     const size_t m = c->m(), n = c->n();
     const int N = c->nx;
     const int P = lspg_cols(n_pod);
-    double *d_b = nullptr, *d_bt = nullptr, *d_btT = nullptr, *d_w = nullptr, *d_wT = nullptr,
+    double *d_b = nullptr, *d_bt = nullptr, *d_btT = nullptr, *d_bk = nullptr, *d_w = nullptr,
+           *d_wT = nullptr,
            *d_wp = nullptr, *d_y = nullptr, *d_part = nullptr, *d_G = nullptr, *d_chunk = nullptr,
            *d_tr = nullptr;
     unsigned *d_err = nullptr;
@@ -2127,7 +2128,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
         dfree(d_info), dfree(d_d0);
         if (registered) (void)hipHostUnregister(snaps);
         for (auto e : evs) (void)hipEventDestroy(e);
-        dfree(d_b), dfree(d_bt), dfree(d_btT), dfree(d_w), dfree(d_wT), dfree(d_wp), dfree(d_y);
+        dfree(d_b), dfree(d_bt), dfree(d_btT), dfree(d_bk), dfree(d_w), dfree(d_wT), dfree(d_wp), dfree(d_y);
         dfree(d_part), dfree(d_G), dfree(d_err), dfree(d_chunk), dfree(d_tr);
     };
     int rc = BURG_OK;
@@ -2166,6 +2167,10 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     for (int p = 0; p < 2 * n_pod; ++p)
         LLAUNCH(launch_basis_transpose(d_bt + (size_t)p * n, d_btT + (size_t)p * n, N, N,
                                        c->stream));
+    if (lspg_gram_blocked(n_pod)) {
+        LCHK(dalloc(&d_bk, lspg_blocked_count(n, n_pod)));
+        LLAUNCH(launch_lspg_block_basis(d_bt, d_btT, n, n_pod, d_bk, c->stream));
+    }
     LCHK(dalloc(&d_w, m));
     LCHK(dalloc(&d_wT, m));
     LCHK(dalloc(&d_wp, m));
@@ -2266,7 +2271,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     LLAUNCH(launch_lspg_project(d_bt, d_wp, n_pod, m, d_part, d_y, c->stream));  // y0 = V^T w0
     LCHK(expand());                                                              // w0 = V y0
     LCHK(keep(0));
-    LspgArgs la{c->cf, d_w, d_wT, d_bt, d_btT, c->d_r, n_pod};
+    LspgArgs la{c->cf, d_w, d_wT, d_bt, d_btT, c->d_r, n_pod, d_bk};
     int64_t total_its = 0;
     for (int s = 0; s < num_steps; ++s) {
         LHIP(hipMemcpyAsync(d_wp, d_w, m * sizeof(double), hipMemcpyDeviceToDevice, c->stream));

@@ -24,6 +24,9 @@
 // basis are kept in both layouts) and S the row below in the transposed plane.
 #include "burg_internal.h"
 
+#include <cstdlib>
+#include <cstring>
+
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 #include <rocsolver/rocsolver.h>
@@ -209,7 +212,7 @@ __global__ __launch_bounds__(kLB) void lspg_gram_kernel(LspgArgs a, double *__re
 constexpr int kMC = 32;
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-template <int NB>
+template <int NB, int CH>
 __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double *__restrict__ partial)
 {
     constexpr int P = 16 * NB;
@@ -242,6 +245,10 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
     const int j = tid & (kMC - 1), kg = tid / kMC;  // fill role: cell j, columns kg + 8 q
     const int orow = lane >> 4, ocol = lane & 15;    // MFMA operand role
     const size_t ntiles = (n + kMC - 1) / kMC;
+    // columns per filling thread, loaded in chunks of CH: every load of a
+    // chunk is issued before the first LDS store (a store between two loads
+    // would otherwise serialise them -- one memory latency per column)
+    constexpr int KPT = P / (kLB / kMC);
     for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
         const size_t i = t * kMC + j;
         const bool ok = i < n;
@@ -252,19 +259,30 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
         const double *u = a.w, *v = a.w + n, *uT = a.wT, *vT = a.wT + n;
         const double ui = u[ii], vi = v[ii], uW = u[iw], vW = v[iw];
         const double uTi = uT[ii], vTi = vT[ii], uTS = uT[is], vTS = vT[is];
+        const double rui = a.r[ii], rvi = a.r[n + ii];
         const double ax = al * a.cf.inv_dx[c], axw = west ? al * a.cf.inv_dx[c - 1] : 0.0;
         const double ay = al * a.cf.inv_dy[r], ays = south ? al * a.cf.inv_dy[r - 1] : 0.0;
-#pragma unroll 4
-        for (int k = kg; k < P; k += kLB / kMC) {
-            double yu = 0.0, yv = 0.0;
-            if (ok && k < a.npod) {
-                const double *xu = a.bt + (size_t)k * m, *xv = xu + n;
-                const double *xuT = a.btT + (size_t)k * m, *xvT = xuT + n;
-                const double xui = xu[ii], xvi = xv[ii], xuw = xu[iw], xvw = xv[iw];
-                const double xuTi = xuT[ii], xvTi = xvT[ii], xuTS = xuT[is], xvTS = xvT[is];
+#pragma unroll
+        for (int q0 = 0; q0 < KPT; q0 += CH) {
+            double xl[CH][8];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const int k = kg + (kLB / kMC) * (q0 + q);
+                const int kk = k < a.npod ? k : a.npod - 1;  // always a valid plane
+                const double *xu = a.bt + (size_t)kk * m, *xv = xu + n;
+                const double *xuT = a.btT + (size_t)kk * m, *xvT = xuT + n;
+                xl[q][0] = xu[ii], xl[q][1] = xv[ii], xl[q][2] = xu[iw], xl[q][3] = xv[iw];
+                xl[q][4] = xuT[ii], xl[q][5] = xvT[ii], xl[q][6] = xuT[is], xl[q][7] = xvT[is];
+            }
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+                const int k = kg + (kLB / kMC) * (q0 + q);
+                if (q0 + q >= KPT) break;
+                const double xui = xl[q][0], xvi = xl[q][1], xuw = xl[q][2], xvw = xl[q][3];
+                const double xuTi = xl[q][4], xvTi = xl[q][5], xuTS = xl[q][6], xvTS = xl[q][7];
                 const double mT = vTi * xuTi + uTi * xvTi;
-                yu = xui + ax * (ui * xui) + 0.5 * ay * mT;
-                yv = xvi + ay * (vTi * xvTi) + 0.5 * ax * (vi * xui + ui * xvi);
+                double yu = xui + ax * (ui * xui) + 0.5 * ay * mT;
+                double yv = xvi + ay * (vTi * xvTi) + 0.5 * ax * (vi * xui + ui * xvi);
                 if (west) {
                     yu -= axw * (uW * xuw);
                     yv -= 0.5 * axw * (vW * xuw + uW * xvw);
@@ -273,12 +291,20 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
                     yu -= 0.5 * ays * (vTS * xuTS + uTS * xvTS);
                     yv -= ays * (vTS * xvTS);
                 }
-            } else if (ok && k == a.npod) {
-                yu = -a.r[ii];
-                yv = -a.r[n + ii];
+                if (k == a.npod) {
+                    yu = -rui;
+                    yv = -rvi;
+                } else if (k > a.npod) {
+                    yu = 0.0;
+                    yv = 0.0;
+                }
+                if (!ok) {
+                    yu = 0.0;
+                    yv = 0.0;
+                }
+                X[j * LD + k] = yu;
+                X[(kMC + j) * LD + k] = yv;
             }
-            X[j * LD + k] = yu;
-            X[(kMC + j) * LD + k] = yv;
         }
         __syncthreads();
 #pragma unroll 4
@@ -304,6 +330,176 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
             out[(size_t)rr * P + cc] = acc[q][e];
             if (pb1[q] != pb2[q]) out[(size_t)cc * P + rr] = acc[q][e];
         }
+    }
+}
+
+// Warp-specialised variant (default for P <= 96): 8 waves, waves 4..7 fill
+// the X tile of the NEXT tile while waves 0..3 run the MFMAs on the current
+// one, through two LDS buffers and one barrier per tile.  A filling thread
+// issues the loads of all its KPT basis columns (8 each) before its first
+// LDS store (in two halves at P = 96: the register budget of two waves per
+// SIMD), so a tile costs one or two memory latencies, not one per column;
+// the products and the Gram blocks are those of lspg_gram_mfma_kernel.
+template <int NB>
+__global__ __launch_bounds__(2 * kLB) void lspg_gram_ws_kernel(LspgArgs a, double *__restrict__ partial)
+{
+    constexpr int P = 16 * NB;
+    constexpr int LD = P + 17;
+    constexpr int NPAIR = NB * (NB + 1) / 2;
+    constexpr int NQ = (NPAIR + 3) / 4;
+    constexpr int XS = 2 * kMC * LD;       // doubles per buffer
+    constexpr int KPT = P / (kLB / kMC);   // basis columns per filling thread
+    constexpr int CH = KPT > 8 ? KPT / 2 : KPT;  // loaded together (register budget)
+    extern __shared__ double gram_lds[];   // two buffers of XS (dynamic)
+    const int N = a.cf.nx;
+    const size_t n = (size_t)N * N;
+    const double al = a.cf.alpha;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const size_t ntiles = (n + kMC - 1) / kMC, ng = gridDim.x;
+    const size_t cnt = blockIdx.x < ntiles ? (ntiles - 1 - blockIdx.x) / ng + 1 : 0;
+
+    if (wv >= 4) {
+        // ---- fill role: cell j of the tile, basis columns kg + 8 q
+        const int ft = tid - kLB;
+        const int j = ft & (kMC - 1), kg = ft / kMC;
+        for (size_t it = 0; it <= cnt; ++it) {
+            if (it < cnt) {
+                double *X = gram_lds + (it & 1) * XS;
+                const size_t i = (blockIdx.x + it * ng) * kMC + j;
+                const bool ok = i < n;
+                const size_t ii = ok ? i : n - 1;
+                const int r = (int)(ii / N), c = (int)(ii - (size_t)r * N);
+                const bool west = c > 0, south = r > 0;
+                const size_t iw = west ? ii - 1 : ii, is = south ? ii - N : ii;
+                // blocked basis: cell i, column k, array e (xu, xv, xuT, xvT) at
+                // ((i / 32 * npod + k) * 4 + e) * 32 + i % 32 -- one tile's values
+                // for all columns are one contiguous run (few pages, full lines)
+                const size_t np = (size_t)a.npod;
+                const double *bi = a.bk + (ii / kMC) * np * 128 + (ii % kMC);
+                const double *bw = a.bk + (iw / kMC) * np * 128 + (iw % kMC);
+                const double *bs = a.bk + (is / kMC) * np * 128 + (is % kMC) + 64;
+                const double *u = a.w, *v = a.w + n, *uT = a.wT, *vT = a.wT + n;
+                const double ui = u[ii], vi = v[ii], uW = u[iw], vW = v[iw];
+                const double uTi = uT[ii], vTi = vT[ii], uTS = uT[is], vTS = vT[is];
+                const double rui = a.r[ii], rvi = a.r[n + ii];
+                const double ax = al * a.cf.inv_dx[c], axw = west ? al * a.cf.inv_dx[c - 1] : 0.0;
+                const double ay = al * a.cf.inv_dy[r], ays = south ? al * a.cf.inv_dy[r - 1] : 0.0;
+#pragma unroll
+                for (int q0 = 0; q0 < KPT; q0 += CH) {
+                    double xl[CH][8];
+#pragma unroll
+                    for (int q = 0; q < CH; ++q) {
+                        const int k = kg + (kLB / kMC) * (q0 + q);
+                        const size_t ko = (size_t)(k < a.npod ? k : a.npod - 1) * 128;  // valid column
+                        xl[q][0] = bi[ko], xl[q][1] = bi[ko + 32], xl[q][2] = bw[ko], xl[q][3] = bw[ko + 32];
+                        xl[q][4] = bi[ko + 64], xl[q][5] = bi[ko + 96], xl[q][6] = bs[ko], xl[q][7] = bs[ko + 32];
+                    }
+#pragma unroll
+                    for (int q = 0; q < CH; ++q) {
+                        const int k = kg + (kLB / kMC) * (q0 + q);
+                        const double xui = xl[q][0], xvi = xl[q][1], xuw = xl[q][2], xvw = xl[q][3];
+                        const double xuTi = xl[q][4], xvTi = xl[q][5], xuTS = xl[q][6], xvTS = xl[q][7];
+                        const double mT = vTi * xuTi + uTi * xvTi;
+                        double yu = xui + ax * (ui * xui) + 0.5 * ay * mT;
+                        double yv = xvi + ay * (vTi * xvTi) + 0.5 * ax * (vi * xui + ui * xvi);
+                        if (west) {
+                            yu -= axw * (uW * xuw);
+                            yv -= 0.5 * axw * (vW * xuw + uW * xvw);
+                        }
+                        if (south) {
+                            yu -= 0.5 * ays * (vTS * xuTS + uTS * xvTS);
+                            yv -= ays * (vTS * xvTS);
+                        }
+                        if (k == a.npod) {
+                            yu = -rui;
+                            yv = -rvi;
+                        } else if (k > a.npod) {
+                            yu = 0.0;
+                            yv = 0.0;
+                        }
+                        if (!ok) {
+                            yu = 0.0;
+                            yv = 0.0;
+                        }
+                        X[j * LD + k] = yu;
+                        X[(kMC + j) * LD + k] = yv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+    // ---- MFMA role: this wave's block pairs (upper triangle, row-major)
+    int pb1[NQ], pb2[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        int p = wv + 4 * q, b1 = 0;
+        if (p >= NPAIR) p = -1;
+        int rem = p;
+        while (rem >= 0 && rem >= NB - b1) {
+            rem -= NB - b1;
+            ++b1;
+        }
+        pb1[q] = p < 0 ? -1 : b1;
+        pb2[q] = p < 0 ? -1 : b1 + rem;
+    }
+    dbl4 acc[NQ];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) acc[q] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int orow = lane >> 4, ocol = lane & 15;
+    for (size_t it = 0; it <= cnt; ++it) {
+        if (it >= 1) {
+            const double *X = gram_lds + ((it - 1) & 1) * XS;
+#pragma unroll 4
+            for (int s4 = 0; s4 < 2 * kMC; s4 += 4) {
+                const double *xr = X + (s4 + orow) * LD + ocol;
+#pragma unroll
+                for (int q = 0; q < NQ; ++q) {
+                    if (pb1[q] < 0) continue;
+                    const double av = xr[16 * pb1[q]], bv = xr[16 * pb2[q]];
+                    acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[q], 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    double *out = partial + (size_t)blockIdx.x * P * P;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        if (pb1[q] < 0) continue;
+        const int r0 = 16 * pb1[q], c0 = 16 * pb2[q];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const int rr = r0 + orow + 4 * e, cc = c0 + ocol;
+            out[(size_t)rr * P + cc] = acc[q][e];
+            if (pb1[q] != pb2[q]) out[(size_t)cc * P + rr] = acc[q][e];
+        }
+    }
+}
+
+// Blocked basis for the warp-specialised Gram kernel: bk[((t npod + k) 4 + e)
+// 32 + j] = array e (xu, xv, xuT, xvT) of basis column k at cell 32 t + j
+// (zero past the last cell).  Built once per LSPG run from bt / btT.
+__global__ __launch_bounds__(kLB) void lspg_block_basis_kernel(const double *__restrict__ bt,
+                                                               const double *__restrict__ btT,
+                                                               size_t n, int npod,
+                                                               double *__restrict__ bk)
+{
+    const size_t ntiles = (n + kMC - 1) / kMC;
+    const size_t total = ntiles * (size_t)npod * 128;
+    const size_t m = 2 * n;
+    for (size_t o = (size_t)blockIdx.x * kLB + threadIdx.x; o < total; o += (size_t)gridDim.x * kLB) {
+        const int j = (int)(o & 31), e = (int)((o >> 5) & 3);
+        const size_t tk = o >> 7;
+        const size_t t = tk / npod, k = tk - t * npod;
+        const size_t i = t * kMC + j;
+        double x = 0.0;
+        if (i < n) {
+            const double *src = (e < 2 ? bt : btT) + k * m + (e & 1) * n;
+            x = src[i];
+        }
+        bk[o] = x;
     }
 }
 
@@ -410,14 +606,91 @@ __global__ __launch_bounds__(kLB) void lspg_finish_kernel(const double *__restri
 
 constexpr int kMfmaGroups = 512;  // 2 per CU (57 KB of LDS each at P = 96)
 constexpr int kSumSlices = 16;
+constexpr size_t kMaxGramGroups = 1024;  // partial buffers are sized for this many
+
+// basis columns per load chunk of the Gram kernel's fill (BURG_LSPG_CH: 3, 4
+// or 6 at P = 96 -- a tuning knob; 4 by default)
+int gram_chunk()
+{
+    static int v = 0;
+    if (!v) {
+        v = 4;
+        if (const char *e = std::getenv("BURG_LSPG_CH")) {
+            const int x = std::atoi(e);
+            if (x == 3 || x == 6) v = x;
+        }
+    }
+    return v;
+}
 
 // the MFMA kernel serves P <= 96 (npod <= 95); P = 128 uses the vector kernel
 bool use_mfma(int P) { return P <= 96; }
 
+// BURG_LSPG_GRAM=split selects the one-role MFMA kernel (fill, then MFMA)
+bool gram_ws()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = std::getenv("BURG_LSPG_GRAM");
+        v = (e && std::strcmp(e, "split") == 0) ? 0 : 1;
+    }
+    return v == 1;
+}
+
+size_t gram_ws_lds(int P) { return sizeof(double) * 2 * 2 * kMC * (size_t)(P + 17); }
+
+const void *gram_fn(int P)
+{
+    if (gram_ws()) {
+        switch (P) {
+        case 32: return (const void *)lspg_gram_ws_kernel<2>;
+        case 64: return (const void *)lspg_gram_ws_kernel<4>;
+        case 96: return (const void *)lspg_gram_ws_kernel<6>;
+        default: break;
+        }
+    }
+    switch (P) {
+    case 32: return (const void *)lspg_gram_mfma_kernel<2, 4>;
+    case 64: return (const void *)lspg_gram_mfma_kernel<4, 4>;
+    case 96:
+        return gram_chunk() == 6   ? (const void *)lspg_gram_mfma_kernel<6, 6>
+               : gram_chunk() == 3 ? (const void *)lspg_gram_mfma_kernel<6, 3>
+                                   : (const void *)lspg_gram_mfma_kernel<6, 4>;
+    case 128: return (const void *)lspg_gram_kernel<8>;
+    default: return nullptr;
+    }
+}
+
+bool is_ws(int P) { return gram_ws() && P <= 96; }
+int gram_threads(int P) { return is_ws(P) ? 2 * kLB : kLB; }
+size_t gram_dyn(int P) { return is_ws(P) ? gram_ws_lds(P) : 0; }
+bool gram_prepare(const void *fn, int P)
+{
+    if (!is_ws(P)) return true;
+    return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)gram_dyn(P)) ==
+           hipSuccess;
+}
+
+// one resident wave of workgroups (occupancy x CUs; BURG_LSPG_GROUPS
+// overrides), at most one per tile
 int groups_for(size_t n, int P)
 {
     const size_t cells = use_mfma(P) ? kMC : kGC;
-    const size_t cap = use_mfma(P) ? kMfmaGroups : kGroups;
+    size_t cap = use_mfma(P) ? kMfmaGroups : kGroups;
+    int dev = 0, ncu = 0, per = 0;
+    if (const void *fn = gram_fn(P))
+        if (hipGetDevice(&dev) == hipSuccess &&
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+            gram_prepare(fn, P) &&
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, gram_threads(P), gram_dyn(P)) ==
+                hipSuccess &&
+            per > 0)
+            cap = (size_t)per * ncu;
+    if (const char *e = std::getenv("BURG_LSPG_GROUPS")) {
+        const long v = std::atol(e);
+        if (v > 0 && v <= 4096) cap = (size_t)v;
+    }
+    if (cap > kMaxGramGroups) cap = kMaxGramGroups;
     const size_t tiles = (n + cells - 1) / cells;
     return (int)(tiles < cap ? tiles : cap);
 }
@@ -434,7 +707,7 @@ int lspg_cols(int npod)
 size_t lspg_partial_count(int nx, int npod)
 {
     const int P = lspg_cols(npod);
-    return (size_t)(groups_for((size_t)nx * nx, P) + kSumSlices) * P * P + (size_t)npod * 256;
+    return (size_t)(kMaxGramGroups + kSumSlices) * P * P + (size_t)npod * 256;
 }
 
 int launch_lspg_expand(const double *bt, const double *y, int npod, size_t m, double *w,
@@ -456,17 +729,31 @@ int launch_lspg_project(const double *bt, const double *x, int npod, size_t m, d
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
+bool lspg_gram_blocked(int npod) { return is_ws(lspg_cols(npod)); }
+
+size_t lspg_blocked_count(size_t n, int npod) { return (n + kMC - 1) / kMC * (size_t)npod * 128; }
+
+int launch_lspg_block_basis(const double *bt, const double *btT, size_t n, int npod, double *bk,
+                            hipStream_t st)
+{
+    const size_t total = lspg_blocked_count(n, npod);
+    size_t g = (total + kLB - 1) / kLB;
+    if (g > 65536) g = 65536;
+    hipLaunchKernelGGL(lspg_block_basis_kernel, dim3((unsigned)g), dim3(kLB), 0, st, bt, btT, n,
+                       npod, bk);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
 int launch_lspg_gram(const LspgArgs &a, double *partial, double *G, hipStream_t st)
 {
     const int P = lspg_cols(a.npod);
     const int ng = groups_for((size_t)a.cf.nx * a.cf.nx, P);
-    switch (P) {
-    case 32: hipLaunchKernelGGL(lspg_gram_mfma_kernel<2>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    case 64: hipLaunchKernelGGL(lspg_gram_mfma_kernel<4>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    case 96: hipLaunchKernelGGL(lspg_gram_mfma_kernel<6>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    case 128: hipLaunchKernelGGL(lspg_gram_kernel<8>, dim3(ng), dim3(kLB), 0, st, a, partial); break;
-    default: return -1;
-    }
+    const void *fn = gram_fn(P);
+    if (!fn || !gram_prepare(fn, P) || (is_ws(P) && !a.bk)) return -1;
+    LspgArgs args = a;
+    void *kargs[] = {&args, &partial};
+    if (hipLaunchKernel(fn, dim3(ng), dim3(gram_threads(P)), kargs, gram_dyn(P), st) != hipSuccess)
+        return -3;
     // two-level deterministic reduction of the per-workgroup partials
     const int PP = P * P;
     double *mid = partial + (size_t)ng * PP;
