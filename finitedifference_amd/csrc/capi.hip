@@ -1,6 +1,7 @@
 // capi.hip -- C ABI (include/burgers.h) of libburgers_hip.so: contexts, the
 // time loop (inviscid_burgers_implicit2D, C/hypernet2D.py:72-131) and the
 // parity hooks.  Host-side only; kernels live in march.hip / stencil.hip.
+#include <rocprofiler-sdk-roctx/roctx.h>
 #include <hip/hip_runtime.h>
 #include <rocblas/rocblas.h>
 
@@ -80,6 +81,17 @@ void dfree(T *&p)
 }
 
 }  // namespace
+
+// ROCTx ranges around the ABI entry points and the march launches
+// (rocprofv3 --marker-trace shows them on the timeline; without a profiler
+// attached they cost a call each).
+struct TraceRange {
+    explicit TraceRange(const char *name) { roctxRangePushA(name); }
+    ~TraceRange() { roctxRangePop(); }
+    TraceRange(const TraceRange &) = delete;
+    TraceRange &operator=(const TraceRange &) = delete;
+};
+#define BURG_TRACE(name) TraceRange burg_trace_range_(name)
 
 struct burg_ctx {
     int device = 0;
@@ -527,6 +539,7 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
 
 int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
 {
+    BURG_TRACE("march launch");
     const bool pipe = c->eng_eff == BURG_ENGINE_PIPE;
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
@@ -1293,6 +1306,7 @@ int burg_set_engine(burg_ctx *c, int engine, int stream_w, int tiles_target)
 
 int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, double *norm)
 {
+    BURG_TRACE("burg_residual");
     if (int e = check_ready(c)) return e;
     if (!w || !wp || !r) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
@@ -1309,6 +1323,7 @@ int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, dou
 
 int burg_jvp(burg_ctx *c, const double *w, const double *x, double *y)
 {
+    BURG_TRACE("burg_jvp");
     if (int e = check_ready(c)) return e;
     if (!w || !x || !y) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
@@ -1323,6 +1338,7 @@ int burg_jvp(burg_ctx *c, const double *w, const double *x, double *y)
 
 int burg_block_solve(burg_ctx *c, const double *w, const double *rhs, double *delta)
 {
+    BURG_TRACE("burg_block_solve");
     if (int e = check_ready(c)) return e;
     if (!w || !rhs || !delta) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
@@ -1392,6 +1408,7 @@ int burg_kernel_bench(burg_ctx *c, int which, int reps, double *avg_ms)
 
 int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
 {
+    BURG_TRACE("burg_advance");
     if (int e = check_ready(c)) return e;
     if (num_steps < 0) return fail(BURG_EINVAL, "num_steps < 0");
     if (solver != BURG_SOLVER_MARCH && solver != BURG_SOLVER_NEWTON)
@@ -1437,6 +1454,7 @@ int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
 
 int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st)
 {
+    BURG_TRACE("burg_trajectory");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (c->engine == BURG_ENGINE_TILES)
@@ -1447,6 +1465,7 @@ int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st
 int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,
                double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *st)
 {
+    BURG_TRACE("burg_sweep");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (nmu < 1) return fail(BURG_EINVAL, "nmu must be >= 1");
@@ -1629,6 +1648,7 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
 int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const double *prev_states,
                      int n_pod, const double *basis, double *C, burg_stats *st)
 {
+    BURG_TRACE("burg_ecsw_matrix");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (n_snaps < 1 || n_pod < 1) return fail(BURG_EINVAL, "n_snaps and n_pod must be >= 1");
@@ -1718,6 +1738,7 @@ static int check_device_ptr(const burg_ctx *c, const void *p, const char *what)
 int burg_ecsw_block_device(burg_ctx *c, const double *d_state, const double *d_prev, int n_pod,
                            const double *d_basis_t, double *d_C, float *kernel_ms)
 {
+    BURG_TRACE("burg_ecsw_block_device");
     if (int e = check_ready(c)) return e;
     if (kernel_ms) *kernel_ms = 0.f;
     if (n_pod < 1) return fail(BURG_EINVAL, "n_pod must be >= 1");
@@ -1741,6 +1762,7 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
              double newton_rtol, double *snaps, int64_t ld_snaps, int snap_every,
              burg_stats *st, int32_t *step_iters, double *step_rel)
 {
+    BURG_TRACE("burg_run");
     if (int e = check_ready(c)) return e;
     if (!w0) return fail(BURG_EINVAL, "null w0");
     if (num_steps < 0) return fail(BURG_EINVAL, "num_steps < 0");
@@ -1906,6 +1928,7 @@ static std::string npy_header(size_t m, size_t ncols)
 int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, const char *path,
                  burg_stats *st)
 {
+    BURG_TRACE("burg_run_npy");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (!w0 || !path || !*path) return fail(BURG_EINVAL, "null w0 or path");
@@ -2091,6 +2114,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
               int64_t ld_snaps, double *red_coords, int64_t ld_red, int32_t *step_its,
               double *step_rel, double *times_ms, burg_stats *st)
 {
+    BURG_TRACE("burg_lspg");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (times_ms) times_ms[0] = times_ms[1] = times_ms[2] = 0.0;
@@ -2335,12 +2359,14 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
 int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *U, double *sigma,
              double *ms)
 {
+    BURG_TRACE("burg_pod");
     return burg_pod_rsvd(device, m, ns, snaps, k, 0, 0, nullptr, U, sigma, ms);
 }
 
 int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
                   const double *omega, double *U, double *sigma, double *ms)
 {
+    BURG_TRACE("burg_pod_rsvd");
     if (!snaps || !U || !sigma) return fail(BURG_EINVAL, "null array");
     if (omega && (nrand < k || nrand > ns || n_iter < 0))
         return fail(BURG_EINVAL, "burg_pod_rsvd: need k <= nrand <= ns and n_iter >= 0");

@@ -333,22 +333,23 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
     }
 }
 
-// Warp-specialised variant (default for P <= 96): 8 waves, waves 4..7 fill
-// the X tile of the NEXT tile while waves 0..3 run the MFMAs on the current
-// one, through two LDS buffers and one barrier per tile.  A filling thread
+// Warp-specialised variant (default for P <= 96): waves 4..4+FW-1 fill the
+// X tile of the NEXT tile while waves 0..3 run the MFMAs on the current one,
+// through two LDS buffers and one barrier per tile.  A filling thread
 // issues the loads of all its KPT basis columns (8 each) before its first
 // LDS store (in two halves at P = 96: the register budget of two waves per
 // SIMD), so a tile costs one or two memory latencies, not one per column;
 // the products and the Gram blocks are those of lspg_gram_mfma_kernel.
-template <int NB>
-__global__ __launch_bounds__(2 * kLB) void lspg_gram_ws_kernel(LspgArgs a, double *__restrict__ partial)
+template <int NB, int FW>
+__global__ __launch_bounds__(kLB + FW * 64) void lspg_gram_ws_kernel(LspgArgs a, double *__restrict__ partial)
 {
     constexpr int P = 16 * NB;
     constexpr int LD = P + 17;
     constexpr int NPAIR = NB * (NB + 1) / 2;
     constexpr int NQ = (NPAIR + 3) / 4;
     constexpr int XS = 2 * kMC * LD;       // doubles per buffer
-    constexpr int KPT = P / (kLB / kMC);   // basis columns per filling thread
+    constexpr int KS = FW * 64 / kMC;      // column stride of the filling threads
+    constexpr int KPT = P / KS;            // basis columns per filling thread
     constexpr int CH = KPT > 8 ? KPT / 2 : KPT;  // loaded together (register budget)
     extern __shared__ double gram_lds[];   // two buffers of XS (dynamic)
     const int N = a.cf.nx;
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(2 * kLB) void lspg_gram_ws_kernel(LspgArgs a, doubl
     if (wv >= 4) {
         // ---- fill role: cell j of the tile, basis columns kg + 8 q
         const int ft = tid - kLB;
-        const int j = ft & (kMC - 1), kg = ft / kMC;
+        const int j = ft & (kMC - 1), kg = ft / kMC;  // columns kg + KS q
         for (size_t it = 0; it <= cnt; ++it) {
             if (it < cnt) {
                 double *X = gram_lds + (it & 1) * XS;
@@ -389,14 +390,14 @@ __global__ __launch_bounds__(2 * kLB) void lspg_gram_ws_kernel(LspgArgs a, doubl
                     double xl[CH][8];
 #pragma unroll
                     for (int q = 0; q < CH; ++q) {
-                        const int k = kg + (kLB / kMC) * (q0 + q);
+                        const int k = kg + KS * (q0 + q);
                         const size_t ko = (size_t)(k < a.npod ? k : a.npod - 1) * 128;  // valid column
                         xl[q][0] = bi[ko], xl[q][1] = bi[ko + 32], xl[q][2] = bw[ko], xl[q][3] = bw[ko + 32];
                         xl[q][4] = bi[ko + 64], xl[q][5] = bi[ko + 96], xl[q][6] = bs[ko], xl[q][7] = bs[ko + 32];
                     }
 #pragma unroll
                     for (int q = 0; q < CH; ++q) {
-                        const int k = kg + (kLB / kMC) * (q0 + q);
+                        const int k = kg + KS * (q0 + q);
                         const double xui = xl[q][0], xvi = xl[q][1], xuw = xl[q][2], xvw = xl[q][3];
                         const double xuTi = xl[q][4], xvTi = xl[q][5], xuTS = xl[q][6], xvTS = xl[q][7];
                         const double mT = vTi * xuTi + uTi * xvTi;
@@ -637,15 +638,30 @@ bool gram_ws()
     return v == 1;
 }
 
+// fill waves of the P = 96 ws kernel: 8 (each filling thread loads its 6
+// columns at once; 0.96 ms at 1024^2) or 4 (BURG_LSPG_FILL_WAVES=4: 12
+// columns in two halves, 1.03 ms)
+int gram_fill_waves()
+{
+    static int v = 0;
+    if (!v) {
+        const char *e = std::getenv("BURG_LSPG_FILL_WAVES");
+        v = (e && std::atoi(e) == 4) ? 4 : 8;
+    }
+    return v;
+}
+
 size_t gram_ws_lds(int P) { return sizeof(double) * 2 * 2 * kMC * (size_t)(P + 17); }
 
 const void *gram_fn(int P)
 {
     if (gram_ws()) {
         switch (P) {
-        case 32: return (const void *)lspg_gram_ws_kernel<2>;
-        case 64: return (const void *)lspg_gram_ws_kernel<4>;
-        case 96: return (const void *)lspg_gram_ws_kernel<6>;
+        case 32: return (const void *)lspg_gram_ws_kernel<2, 4>;
+        case 64: return (const void *)lspg_gram_ws_kernel<4, 4>;
+        case 96:
+            return gram_fill_waves() == 8 ? (const void *)lspg_gram_ws_kernel<6, 8>
+                                          : (const void *)lspg_gram_ws_kernel<6, 4>;
         default: break;
         }
     }
@@ -662,7 +678,7 @@ const void *gram_fn(int P)
 }
 
 bool is_ws(int P) { return gram_ws() && P <= 96; }
-int gram_threads(int P) { return is_ws(P) ? 2 * kLB : kLB; }
+int gram_threads(int P) { return is_ws(P) ? kLB + 64 * (P == 96 ? gram_fill_waves() : 4) : kLB; }
 size_t gram_dyn(int P) { return is_ws(P) ? gram_ws_lds(P) : 0; }
 bool gram_prepare(const void *fn, int P)
 {

@@ -236,3 +236,24 @@ def test_oracle_pod_vs_reference(orc, tag):
     keep = s > 1e-6 * s[0]
     assert keep.sum() >= 8
     assert np.max(np.abs(u[:, keep] - ur[:, keep])) < 1e-8
+
+
+def test_oracle_under_sanitizers():
+    """Host sanitizers over the CPU oracle (AddressSanitizer +
+    UndefinedBehaviorSanitizer, oracle/sanitize_check.c via `make -C oracle
+    sanitize`): every entry point on a ragged 37 x 23 grid, Newton = march to
+    1e-12, the tile schedule simulator bitwise = the march, the OpenMP sweep,
+    and J x / block solve inverse to each other; any sanitizer report fails."""
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    odir = os.path.join(os.path.dirname(here), "oracle")
+    b = subprocess.run(["make", "-s", "-C", odir, "sanitize"], capture_output=True, text=True)
+    if b.returncode != 0 and "asan" in (b.stderr + b.stdout).lower():
+        pytest.skip("no sanitizer runtime for this compiler: " + b.stderr[-200:])
+    assert b.returncode == 0, b.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", OMP_NUM_THREADS="2")
+    r = subprocess.run([os.path.join(odir, "_san", "sanitize_check")], capture_output=True,
+                       text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sanitize_check ok" in r.stdout
