@@ -1046,8 +1046,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         const int sm_ = sb & (W - 1);
         const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
+        // (the top lane's column must not wrap inside the block: a halo ring
+        // row is the whole slab width, so ncol_real alone would let the
+        // SGPR offset run on into the next tile's columns)
         const bool steady = WIDE && nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
-                            ct0 + U <= ncol_real;
+                            ct0 + U <= min(W, ncol_real);
         if (steady)
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {

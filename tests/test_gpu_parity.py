@@ -543,6 +543,30 @@ def test_slab_wide_rows_two_processes_one_gpu(gpu, orc, tmp_path):
         assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
 
 
+@pytest.mark.parametrize("W,N,T", [(128, 1024, 12), (256, 1024, 6), (1024, 2048, 2)])
+def test_slab_wide_tile_steady_blocks_two_processes_one_gpu(gpu, orc, tmp_path, W, N, T):
+    """Slabs whose tiles run the steady / steady-edge blocks (W > 64) on the
+    strips that write the halo ring -- the multi-GPU bench's tiling (W = 256
+    at 4096 x 4096 per GPU).  The halo ring's row is the whole slab width, so
+    a steady block must still stop at its own tile's last column (a block
+    that ran on into the next tile's slots stalled both ranks at step 0).
+    Two processes share the GPU (W forced, both grids resident); the
+    assembled trajectory is the single-domain march bit for bit."""
+    world = 2
+    dt = 0.05 * 1024 / N
+    _run_slabs(tmp_path, N, T, world, SLAB_W=W, SLAB_DT=repr(dt))
+    widths = {open(os.path.join(tmp_path, f"slab{r}.w")).read() for r in range(world)}
+    assert widths == {str(W)}, widths
+    assert _halo_modes(tmp_path, world) == [(0, 2), (2, 0)]
+    from finitedifference_amd.dist import assemble_snaps
+    parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
+    snaps = assemble_snaps(parts, N, N)
+    P = orc.Problem(N, dt=dt)
+    ref, _, _ = P.fom(np.ones(P.m), T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+
+
 def test_fine750_eight_uneven_slabs_one_gpu(gpu, orc, tmp_path):
     """SURVEY.md 8(d) C5 parity case on one GPU: 750^2 over 8 slab processes
     (uneven 94/93-row slabs), 500 steps with snap_every=100: assembled
