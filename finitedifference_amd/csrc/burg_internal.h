@@ -110,7 +110,7 @@ struct StreamArgs {
 // use two sentinel colours so that a slot's emptiness is tied to a step.
 constexpr int kPipeR = 8;   // global mailbox slots (steps) per edge, power of two
 constexpr int kPipeRL = 4;  // LDS ring slots (steps) per intra-workgroup edge
-constexpr int kPipeSweepMax = 10;  // trajectories per sweep launch (LDS-resident tables)
+constexpr int kPipeSweepMax = 9;   // trajectories per sweep launch (LDS-resident tables)
 
 struct PipeArgs {
     Coeffs cf;

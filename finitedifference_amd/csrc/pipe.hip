@@ -212,6 +212,10 @@ __device__ __forceinline__ void st_sys_so(__amdgpu_buffer_rsrc_t rs, unsigned vo
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 17);
 }
+__device__ __forceinline__ void st_plain_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
+}
 __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
@@ -269,14 +273,18 @@ struct PipeLds {
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
-    v4u cc[4][W + (WIDE ? 8 : 0)];  // per wave: {hx, src} of the tile's columns (wide: + the
-                                    // first 8 again, so a block's lane reads base + u unwrapped)
+    v4u cc[4][W + (W == 8 ? 0 : 8)];  // per wave: {hx, src} of the tile's columns, + the
+                                      // first 8 again, so a steady block's lane reads
+                                      // base + u unwrapped (W = 8: no steady blocks)
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
-    v4u zeros[WIDE ? 8 : 1];  // wide: the south inflow of a boundary strip, read by block offsets
-    v4u dump[WIDE ? kWave : 1];  // wide: write target of lanes with nothing to hand off (shared)
+    v4u zeros[WIDE ? 8 : W == 8 ? 1 : BURG_NARROW_U];  // south inflow of a boundary strip,
+                                                       // read by block offsets
+    // write target of lanes with nothing to hand off (W = 8 runs no steady
+    // blocks: its image must fit three times in a CU)
+    v4u dump[W == 8 ? 1 : kWave];
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
@@ -297,6 +305,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     constexpr int kThreads = threads_of<W>();
     static_assert(!is_wide<W>() || sizeof(PipeLds<W, SWEEP>::win) <= 65536,
                   "LDS-DMA window must sit below 64 KB");
+    static_assert(sizeof(PipeLds<W, SWEEP>) <= 160 * 1024, "LDS image exceeds the CU's 160 KiB");
     constexpr bool WIDE = is_wide<W>();
     // three narrow W=8 workgroups per CU: room for 8 slab processes sharing one
     // GPU (the 750^2 C5 case, tests/test_gpu_parity.py) with all grids resident
@@ -370,8 +379,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         sm.filled[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
-    if constexpr (WIDE)
-        if (threadIdx.x < 8) sm.zeros[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
+    if (threadIdx.x < (WIDE ? 8 : W == 8 ? 1 : BURG_NARROW_U)) sm.zeros[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
     if constexpr (SWEEP) {
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
-        for (int c = lane; c < W + (WIDE ? 8 : 0); c += kWave) {
+        for (int c = lane; c < W + (W == 8 ? 0 : 8); c += kWave) {
             const d2 v = a.colc[(size_t)(tj0 + wave) * W + (c & (W - 1))];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
@@ -727,18 +735,29 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // into the LDS instructions' immediate fields.
     struct Bases {
         LDS v4u *wb, *cb, *ib;
+        int c0;  // the lane's column at the block's first diagonal
     };
     auto bases_of = [&](int sb) -> Bases {
         Bases b;
-        b.wb = &sm.win[k][sb % KWIN][lane];
+        // narrow tiles: the lane's previous states in st (slot s mod W; a block
+        // starts at a multiple of U, so sb + u does not wrap)
+        if constexpr (WIDE) b.wb = &sm.win[k][sb % KWIN][lane];
+        else b.wb = (LDS v4u *)&my_st[(sb & (W - 1)) * kWave + lane];
         b.cb = &sm.cc[k][(sb - lane) & (W - 1)];
         b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : &sm.zeros[0];
+        b.c0 = (sb - lane) & (W - 1);
         return b;
     };
     auto fetch_b = [&](const Bases &b, int u) -> In {
         In in;
         in.nt = false;
         in.src = 0.0;
+        if constexpr (SWEEP) {
+            // the trajectory's source by column: the lane's column wraps to 0
+            // at diagonal se_uw of the block (the table is not padded)
+            const int c = ((b.c0 + u) & (W - 1));
+            in.src = src_cur[c];
+        }
         in.xs = lds_ld(b.wb + u * kWave);
         in.cs = b.cb[u];
         in.gw = v4u{0u, 0u, 0u, 0u};
@@ -856,13 +875,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // ---- outputs (lanes that have not started keep their step-0 state)
         const v4u out = as_v4u(o0, o1);
         if constexpr (!WIDE) {
-            if (t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
+            if (STEADY || t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
         }
         // wide tiles: the loader wave reads this entry back (sc1 DMA) W
         // diagonals later, so it is stored write-through to L2 (sc1): the
         // store's vmcnt then completes at L2, which the done[] protocol needs
         if constexpr (STEADY) {
-            st_dev_so(ring, lane16, pw * 1024u, out);
+            if constexpr (WIDE) st_dev_so(ring, lane16, pw * 1024u, out);
+            else st_plain_so(ring, lane16, pw * 1024u, out);
             ++pw;  // (no wrap inside a steady block)
         } else {
             if constexpr (WIDE) st_dev(ring, valid ? pw * 1024u + lane16 : kOOB, out);
@@ -883,8 +903,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // wide tiles issue every store on every diagonal (out-of-range offsets
         // are dropped): exactly 3 per edge and 2 per interior diagonal, which
         // the vmcnt of done[] counts
-        if constexpr (SE)
-            st_dev(wbox, atE ? se_eoff : kOOB, eo);
+        if constexpr (SE) {
+            // (wide: every diagonal issues the same number of stores, for done[])
+            if (WIDE || east_glob) st_dev(wbox, atE ? se_eoff : kOOB, eo);
+        }
         else if (EDGE && (WIDE || east_glob))
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
         if (WIDE || has_north) {
@@ -903,15 +925,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 st_sys(nrs, off, no);
             }
         }
-        // consumed inbound slots back to empty
-        if constexpr (WIDE) {
+        // consumed inbound slots back to empty (steady-edge blocks: once per
+        // block, run_block)
+        if constexpr (WIDE || STEADY) {
             if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane], lempty);
             // (the south slots are freed once per block, run_block)
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
             if (need_s && lane == 0) lds_st(&sm.ins[k][s & (kNI - 1)], lempty);
         }
-        if constexpr (SWEEP) {
+        if constexpr (SWEEP && !STEADY) {
             // the lane finished the first step of its next trajectory: switch
             if (in.nt && atE) {
                 ++jl;
@@ -932,14 +955,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // diagonal: a lane's trajectory switch (in diagonal s) decides which
     // state and source table diagonal s + 1 reads.
     auto run_block = [&](auto tag, const int sb) {
-        if constexpr (SWEEP) {
+        if constexpr (SWEEP && decltype(tag)::value != 3) {
             In a0 = fetch(tag, sb);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 diagonal(tag, sb + u, u, a0);
                 if (u + 1 < U) a0 = fetch(tag, sb + u + 1);
             }
-        } else if constexpr (!WIDE || decltype(tag)::value == 0) {
+        } else if constexpr ((!WIDE && decltype(tag)::value != 3) || decltype(tag)::value == 0) {
             In a0 = fetch(tag, sb), a1 = fetch(tag, sb + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -979,7 +1002,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (decltype(tag)::value == 3 && has_west)
                 lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane], lempty);
         }
-        if constexpr (WIDE) {
+        if constexpr (WIDE || decltype(tag)::value == 3) {
             // the block's south inbox slots back to empty, one write: lane i
             // frees diagonal sb + i's slot
             if (has_south)
@@ -1049,14 +1072,19 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // (the top lane's column must not wrap inside the block: a halo ring
         // row is the whole slab width, so ncol_real alone would let the
         // SGPR offset run on into the next tile's columns)
-        const bool steady = WIDE && nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
-                            ct0 + U <= min(W, ncol_real);
+        // narrow tiles (U <= W: a lane meets column 0 at most once per block)
+        // run steady-edge blocks too; sweeps only where no lane is in the
+        // first step of its next trajectory (that step reads the initial state)
+        bool steady = nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
+                      ct0 + U <= min(W, ncol_real);
+        if constexpr (SWEEP)
+            steady = steady && !any_lane(((sb + U - 1 - lane) >> LW) >= qn);
         if (steady)
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
             // (narrow-or-equal tiles, W <= 64: one block's lanes span several
             // steps, so the steady offsets do not hold -- plain edge blocks)
-            if (WIDE && W > kWave && steady) run_block(SteadyEdge(), sb);
+            if ((W == 16 || W > kWave) && steady) run_block(SteadyEdge(), sb);
             else run_block(Edge(), sb);
         } else if (steady) {
             run_block(Steady(), sb);
