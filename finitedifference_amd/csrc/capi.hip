@@ -15,7 +15,6 @@
 #include <condition_variable>
 #include <mutex>
 #include <string>
-#include <atomic>
 #include <thread>
 #include <vector>
 
@@ -1995,15 +1994,8 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         cleanup();
         return fail(BURG_EINVAL, "write(%s): %s", path, strerror(errno));
     }
-    // writer threads per block (BURG_NPY_WRITERS, default 8)
-    int nw = 8;
-    if (const char *e = std::getenv("BURG_NPY_WRITERS")) {
-        const int v = std::atoi(e);
-        if (v >= 1 && v <= 64) nw = v;
-    }
-    writer = std::thread([&, nw]() {
+    writer = std::thread([&]() {
         int i = 0;
-        size_t foff = hdr.size();
         for (;;) {
             size_t nbytes = 0;
             {
@@ -2012,32 +2004,17 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
                 if (ready_bytes[i] == 0) return;
                 nbytes = ready_bytes[i];
             }
-            // the block goes to the file as nw slices written in parallel
-            // (pwrite at their own offsets): one thread's copy into the page
-            // cache runs at a few GB/s, well below the pinned D2H
             const char *p = (const char *)h_blk[i];
-            const size_t piece = ((nbytes + nw - 1) / nw + 4095) / 4096 * 4096;
-            std::vector<std::thread> slices;
-            std::atomic<bool> bad{false};
-            for (size_t a = 0; a < nbytes; a += piece) {
-                const size_t len = std::min(piece, nbytes - a);
-                slices.emplace_back([&, a, len]() {
-                    size_t done = 0;
-                    while (done < len) {
-                        const ssize_t wr = pwrite(fd, p + a + done, len - done, (off_t)(foff + a + done));
-                        if (wr <= 0) {
-                            bad = true;
-                            return;
-                        }
-                        done += (size_t)wr;
-                    }
-                });
-            }
-            for (auto &t : slices) t.join();
-            foff += nbytes;
-            if (bad) {
-                std::lock_guard<std::mutex> g(mu);
-                werr = true;
+            size_t left = nbytes;
+            while (left > 0) {
+                const ssize_t wr = write(fd, p, left);
+                if (wr <= 0) {
+                    std::lock_guard<std::mutex> g(mu);
+                    werr = true;
+                    break;
+                }
+                p += wr;
+                left -= (size_t)wr;
             }
             {
                 std::lock_guard<std::mutex> g(mu);

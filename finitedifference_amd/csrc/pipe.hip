@@ -699,7 +699,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     v4u se_gw = v4u{0u, 0u, 0u, 0u};
     LDS v4u *se_eaddr = nullptr;
     unsigned se_eoff = kOOB;
-    unsigned noffs = 0;  // steady blocks: the top lane's north slot offset at the current diagonal
+    // steady blocks: the top lane's north slot offset at the block's first
+    // diagonal, and (noffs2) at column 0 of the next step, reached at
+    // diagonal uwrap of the block (>= U: no wrap in the block)
+    unsigned noffs = 0, noffs2 = 0;
+    int uwrap = U;
     auto fetch = [&](auto edge_tag, int s) -> In {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
@@ -916,8 +920,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const v4u no = as_v4u(on0, on1);
             if constexpr (STEADY) {
                 // the top lane's slot: SGPR offset, advanced one column per diagonal
-                st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, noffs, no);
-                noffs += ncol;
+                if constexpr (WIDE) {
+                    st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, noffs, no);
+                    noffs += ncol;
+                } else {
+                    const unsigned so = u < uwrap ? noffs + (unsigned)u * ncol
+                                                  : noffs2 + (unsigned)(u - uwrap) * ncol;
+                    st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, so, no);
+                }
             } else {
                 const unsigned off = (out_n & (c < ncol_real))
                                          ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
@@ -1069,18 +1079,24 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         const int sm_ = sb & (W - 1);
         const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
-        // (the top lane's column must not wrap inside the block: a halo ring
-        // row is the whole slab width, so ncol_real alone would let the
-        // SGPR offset run on into the next tile's columns)
+        // (narrow tiles: the top lane's column may wrap to the next step
+        // inside the block -- noffs2 -- except on a halo ring, whose row is
+        // the whole slab width (and a partial last tile has fewer real
+        // columns); wide tiles keep the no-wrap condition: the select would
+        // cost more instructions than the 1 in W / U blocks it makes steady)
         // narrow tiles (U <= W: a lane meets column 0 at most once per block)
         // run steady-edge blocks too; sweeps only where no lane is in the
         // first step of its next trajectory (that step reads the initial state)
         bool steady = nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
-                      ct0 + U <= min(W, ncol_real);
+                      ((!WIDE && north_dev) || ct0 + U <= min(W, ncol_real));
         if constexpr (SWEEP)
             steady = steady && !any_lane(((sb + U - 1 - lane) >> LW) >= qn);
         if (steady)
+        {
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
+            noffs2 = nb + (unsigned)((a.qbase + (tt0 >> LW) + 1) & (kR - 1)) * nstep;
+            uwrap = W - ct0;
+        }
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
             // (narrow-or-equal tiles, W <= 64: one block's lanes span several
             // steps, so the steady offsets do not hold -- plain edge blocks)
