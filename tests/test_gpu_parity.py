@@ -543,21 +543,24 @@ def test_slab_wide_rows_two_processes_one_gpu(gpu, orc, tmp_path):
         assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
 
 
-@pytest.mark.parametrize("W,N,T", [(128, 1024, 12), (256, 1024, 6), (1024, 2048, 2)])
-def test_slab_wide_tile_steady_blocks_two_processes_one_gpu(gpu, orc, tmp_path, W, N, T):
+@pytest.mark.parametrize("W,N,T,world", [(128, 1024, 12, 2), (256, 1024, 6, 2), (1024, 2048, 2, 2),
+                                         (128, 768, 10, 3)])
+def test_slab_wide_tile_steady_blocks_two_processes_one_gpu(gpu, orc, tmp_path, W, N, T, world):
     """Slabs whose tiles run the steady / steady-edge blocks (W > 64) on the
     strips that write the halo ring -- the multi-GPU bench's tiling (W = 256
     at 4096 x 4096 per GPU).  The halo ring's row is the whole slab width, so
     a steady block must still stop at its own tile's last column (a block
     that ran on into the next tile's slots stalled both ranks at step 0).
-    Two processes share the GPU (W forced, both grids resident); the
-    assembled trajectory is the single-domain march bit for bit."""
-    world = 2
+    Two or three processes share the GPU (W forced, all grids resident; the
+    middle one of three both reads and writes a halo ring, and 768 / 128 = 6
+    tiles per strip leave its second workgroup half full); the assembled
+    trajectory is the single-domain march bit for bit."""
     dt = 0.05 * 1024 / N
     _run_slabs(tmp_path, N, T, world, SLAB_W=W, SLAB_DT=repr(dt))
     widths = {open(os.path.join(tmp_path, f"slab{r}.w")).read() for r in range(world)}
     assert widths == {str(W)}, widths
-    assert _halo_modes(tmp_path, world) == [(0, 2), (2, 0)]
+    assert _halo_modes(tmp_path, world) == [(0 if r == 0 else 2, 0 if r == world - 1 else 2)
+                                            for r in range(world)]
     from finitedifference_amd.dist import assemble_snaps
     parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
     snaps = assemble_snaps(parts, N, N)

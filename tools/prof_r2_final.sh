@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-2 closing profiles (under gpurun): rocprofv3 kernel stats of the
+# driver's bench command, and the HBM (FETCH_SIZE / WRITE_SIZE) and clock
+# (GRBM_GUI_ACTIVE) passes -- one counter group per run -- of the 4096^2
+# trajectory, the 1024^2 9-mu sweep and the LSPG Gram probe.
+set -o pipefail
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${TAG:-prof_final}
+mkdir -p $O
+cd $R
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_stats.json 2> $O/stats.err || { tail -5 $O/stats.err; exit 1; }
+echo stats ok
+B4="bench.py --steps 3 --warmup 1 --no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e"
+B1="bench.py --nx 1024 --dt 0.05 --sweep 9 --steps 3 --warmup 1 --no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e"
+BL="tools/lspg_probe.py 1024 95 3"
+for name in b4 b1 bl; do
+  case $name in b4) CMD=$B4;; b1) CMD=$B1;; bl) CMD=$BL;; esac
+  for ctr in FETCH_SIZE WRITE_SIZE GRBM_GUI_ACTIVE; do
+    timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d $O/${name}_$ctr -o run -- python3 $CMD > /dev/null 2> $O/${name}_$ctr.err || { tail -5 $O/${name}_$ctr.err; exit 1; }
+    echo "$name $ctr ok"
+  done
+done
+echo PROFOK
