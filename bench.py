@@ -338,6 +338,11 @@ def main():
     from finitedifference_amd.config import get_snapshot_params
     mus = get_snapshot_params()[:args.sweep] if args.sweep > 1 else [MU]
     nmu = len(mus)
+    if nmu == 1:
+        # the trajectory ring (134 GB at 4096^2 x 500 steps) is allocated here,
+        # before the barrier: no rank's first launch waits on a neighbour
+        # still allocating (the halo waits are bounded in time)
+        ctx.reserve(T)
 
     def one_step():
         if nmu == 1:

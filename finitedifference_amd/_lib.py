@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -26,6 +26,7 @@ EXPORTS = (
     "burg_slab_connect", "burg_slab_verify", "burg_slab_halo_note", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
+    "burg_reserve_trajectory",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
     "burg_pod", "burg_pod_rsvd", "burg_run_npy",
 )
@@ -131,6 +132,7 @@ def load(path=None):
             "burg_download_state": (ctypes.c_int, [_VP, _D]),
             "burg_trajectory": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(BurgStats)]),
+            "burg_reserve_trajectory": (ctypes.c_int, [_VP, ctypes.c_int]),
             "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
             "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
             "burg_ecsw_matrix": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int, _D, _D,

@@ -681,13 +681,11 @@ int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
     return 0;
 }
 
-// One device-resident trajectory: num_steps steps from d_state[cur] in ONE
-// launch, every state kept in the ring (HBM) -- the reference's snapshot
-// matrix in ring layout (C/hypernet2D.py:89-126 keeps them all); the final
-// state becomes d_state[cur].  A trajectory whose ring does not fit in 85 % of
-// free HBM (or one descriptor) runs as several launches over a ring of C
-// steps, each launch continuing from the previous one's last states.
-int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats *st)
+// The trajectory ring for num_steps: C steps per launch, L entries.  A ring
+// already sized to the memory limit is reused as it is: the next call would
+// only get the same size back, after a free and a fresh allocation of up to
+// ~240 GB (seconds per call at 8192^2).
+int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_out)
 {
     if (int e = stream_setup(c)) return e;
     if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
@@ -695,9 +693,6 @@ int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats 
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     long long C = std::min(num_steps, stream_max_steps(c));
     const long long have_L = (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave));
-    // a ring already sized to the memory limit is reused as it is: the next
-    // call would only get the same size back, after a free and a fresh
-    // allocation of up to ~240 GB (seconds per call at 8192^2)
     if (C * W + W + 96 > have_L && !(c->ring_maxed && have_L >= 2 * W + 96)) {
         // need a (bigger) ring: size it against free memory
         dfree(c->d_ring);
@@ -714,6 +709,22 @@ int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats 
     }
     const long long L = C * W + W + 96;
     if (int e = ensure_ring(c, L)) return e;
+    *C_out = C;
+    *L_out = L;
+    return 0;
+}
+
+// One device-resident trajectory: num_steps steps from d_state[cur] in ONE
+// launch, every state kept in the ring (HBM) -- the reference's snapshot
+// matrix in ring layout (C/hypernet2D.py:89-126 keeps them all); the final
+// state becomes d_state[cur].  A trajectory whose ring does not fit in 85 % of
+// free HBM (or one descriptor) runs as several launches over a ring of C
+// steps, each launch continuing from the previous one's last states.
+int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats *st)
+{
+    long long C = 0, L = 0;
+    if (int e = trajectory_ring(c, num_steps, &C, &L)) return e;
+    const int W = c->sp.W;
     if (from_initial && !c->d_w0) return fail(BURG_ESTATE, "no uploaded initial state");
     stream_stats_begin(c);
     CHK(launch_ring_load(stream_args(c, L, 0, 0), W, from_initial ? c->d_w0 : c->d_state[c->cur],
@@ -1460,6 +1471,18 @@ int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st
     if (c->engine == BURG_ENGINE_TILES)
         return fail(BURG_EINVAL, "burg_trajectory runs on the stream/pipe engines");
     return stream_trajectory(c, num_steps, from_initial != 0, st);
+}
+
+int burg_reserve_trajectory(burg_ctx *c, int num_steps)
+{
+    BURG_TRACE("burg_reserve_trajectory");
+    if (int e = check_ready(c)) return e;
+    if (c->engine == BURG_ENGINE_TILES)
+        return fail(BURG_EINVAL, "burg_reserve_trajectory serves the stream/pipe engines");
+    long long C = 0, L = 0;
+    if (int e = trajectory_ring(c, num_steps, &C, &L)) return e;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return BURG_OK;
 }
 
 int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,

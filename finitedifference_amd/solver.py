@@ -180,6 +180,12 @@ class FOMContext:
         _lib.check(self._L.burg_download_state(self._h, _lib.dptr(w)))
         return w
 
+    def reserve(self, num_steps):
+        """Allocate the tiling, mailboxes and HBM ring trajectory(num_steps)
+        needs, without launching (burg_reserve_trajectory): multi-GPU ranks
+        call it before the barrier that precedes their first launch."""
+        _lib.check(self._L.burg_reserve_trajectory(self._h, int(num_steps)))
+
     def trajectory(self, num_steps, from_initial=True):
         """num_steps steps in one launch from the uploaded initial state (or,
         from_initial=False, from the resident state), every state kept in HBM;

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 10
+#define BURG_ABI_VERSION 11
 
 enum burg_status {
     BURG_OK = 0,
@@ -225,6 +225,12 @@ int burg_kernel_bench(burg_ctx *ctx, int which, int reps, double *avg_ms);
  * stats->loop_ms is the launch's device time (HIP events on the context's
  * stream). */
 int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *stats);
+/* Allocate (or keep) everything burg_trajectory(ctx, num_steps, ...) needs --
+ * the tiling, the edge mailboxes and the HBM ring of the trajectory (up to
+ * 85 % of free HBM; 134 GB for 500 steps of 4096^2) -- without launching.
+ * Multi-GPU slab ranks call it before the barrier that precedes their first
+ * launch, so no rank's first launch waits for a neighbour's allocation. */
+int burg_reserve_trajectory(burg_ctx *ctx, int num_steps);
 
 /* Parameter sweep (the reference's snapshot generation over a set of mu,
  * e.g. C/run_prom.py:59-71 over get_snapshot_params, C/run_tests.py:38-49):

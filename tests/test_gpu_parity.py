@@ -458,6 +458,26 @@ def test_pipe_4096_trajectory_matches_run(gpu, orc):
     assert np.array_equal(ctx.download(), snaps[:, 1])
 
 
+def test_reserve_then_trajectory(gpu, orc):
+    """burg_reserve_trajectory allocates what burg_trajectory needs without
+    launching (the multi-GPU bench calls it before its barrier); the
+    trajectories that follow -- including a longer one, which grows the
+    ring, and a repeat, which reuses it -- are the oracle's march bit for bit."""
+    N = 200
+    P = orc.Problem(N)
+    ref, _, _ = P.fom(np.ones(P.m), 7)
+    ctx = make_ctx(N)
+    ctx.upload(np.ones(P.m))
+    ctx.reserve(5)
+    ctx.reserve(5)
+    st = ctx.trajectory(5)
+    assert st["engine"] == 2
+    assert np.array_equal(ctx.download(), ref[5])
+    for _ in range(2):
+        ctx.trajectory(7)
+        assert np.array_equal(ctx.download(), ref[7])
+
+
 def test_pipe_8192_chunked_property(gpu, monkeypatch):
     """8192^2 on one GPU (W = 1024, 1024 tiles): a run forced into 2-step
     launches; size-independent property: the last step solves the reference
