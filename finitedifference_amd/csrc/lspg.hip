@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kLB) void lspg_gram_mfma_kernel(LspgArgs a, double 
     }
 }
 
-// Warp-specialised variant (default for P <= 96): waves 4..4+FW-1 fill the
+// Warp-specialised variant (default for every P): waves 4..4+FW-1 fill the
 // X tile of the NEXT tile while waves 0..3 run the MFMAs on the current one,
 // through two LDS buffers and one barrier per tile.  A filling thread
 // issues the loads of all its KPT basis columns (8 each) before its first
@@ -624,7 +624,8 @@ int gram_chunk()
     return v;
 }
 
-// the MFMA kernel serves P <= 96 (npod <= 95); P = 128 uses the vector kernel
+// the one-role MFMA kernel (BURG_LSPG_GRAM=split) serves P <= 96 (npod <= 95);
+// there P = 128 uses the vector kernel
 bool use_mfma(int P) { return P <= 96; }
 
 // BURG_LSPG_GRAM=split selects the one-role MFMA kernel (fill, then MFMA)
@@ -662,6 +663,7 @@ const void *gram_fn(int P)
         case 96:
             return gram_fill_waves() == 8 ? (const void *)lspg_gram_ws_kernel<6, 8>
                                           : (const void *)lspg_gram_ws_kernel<6, 4>;
+        case 128: return (const void *)lspg_gram_ws_kernel<8, 4>;  // (8 fill waves: spills)
         default: break;
         }
     }
@@ -677,7 +679,7 @@ const void *gram_fn(int P)
     }
 }
 
-bool is_ws(int P) { return gram_ws() && P <= 96; }
+bool is_ws(int P) { return gram_ws() && P <= 128; }
 int gram_threads(int P) { return is_ws(P) ? kLB + 64 * (P == 96 ? gram_fill_waves() : 4) : kLB; }
 size_t gram_dyn(int P) { return is_ws(P) ? gram_ws_lds(P) : 0; }
 bool gram_prepare(const void *fn, int P)
@@ -691,8 +693,9 @@ bool gram_prepare(const void *fn, int P)
 // overrides), at most one per tile
 int groups_for(size_t n, int P)
 {
-    const size_t cells = use_mfma(P) ? kMC : kGC;
-    size_t cap = use_mfma(P) ? kMfmaGroups : kGroups;
+    const bool m = use_mfma(P) || is_ws(P);
+    const size_t cells = m ? kMC : kGC;
+    size_t cap = m ? kMfmaGroups : kGroups;
     int dev = 0, ncu = 0, per = 0;
     if (const void *fn = gram_fn(P))
         if (hipGetDevice(&dev) == hipSuccess &&
