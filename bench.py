@@ -198,7 +198,11 @@ def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=None, c
         d = json.load(open(isa_file))[kname]["per_diagonal_averages"]
     except Exception:
         return None
-    if "interior_block" in d:
+    if W <= 16 and "steady_edge_block" in d:
+        # narrow tiles: all but ~1 % of the blocks (the first and last 64
+        # diagonals, a sweep's trajectory starts) are steady-edge blocks
+        cyc, ins = d["steady_edge_block"]["issue_cycles"], d["steady_edge_block"]["total"]
+    elif "interior_block" in d:
         # interior blocks of full strips run the steady variant when built
         inner = d.get("steady_block", d["interior_block"])
         edge = d.get("steady_edge_block", d["edge_block"])

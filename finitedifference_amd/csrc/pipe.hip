@@ -68,7 +68,16 @@
 #include "burg_internal.h"
 #include "cell_math.h"
 
+// pipe_narrow.hip includes this file with BURG_PIPE_NARROW_TU = 1: it
+// compiles the narrow-tile kernels (W = 8, 16) with the default machine
+// scheduler, this unit the wide ones with max-ilp (profiles/r02/sched/: each
+// strategy wins on its own width class)
+#ifndef BURG_PIPE_NARROW_TU
+#define BURG_PIPE_NARROW_TU 0
+#endif
+
 namespace burg {
+const void *pipe_narrow_fn(int W, bool sweep);  // pipe_narrow.hip
 namespace {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -212,15 +221,15 @@ __device__ __forceinline__ void st_sys_so(__amdgpu_buffer_rsrc_t rs, unsigned vo
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 17);
 }
-__device__ __forceinline__ void st_plain_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
+[[maybe_unused]] __device__ __forceinline__ void st_plain_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
 }
-__device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
+[[maybe_unused]] __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
 }
-__device__ __forceinline__ v4u ld_plain(__amdgpu_buffer_rsrc_t rs, unsigned off)
+[[maybe_unused]] __device__ __forceinline__ v4u ld_plain(__amdgpu_buffer_rsrc_t rs, unsigned off)
 {
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
 }
@@ -1126,6 +1135,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
 }
 
+#if BURG_PIPE_NARROW_TU
+}  // namespace
+
+const void *pipe_narrow_fn(int W, bool sweep)
+{
+    if (sweep) return W == 8 ? (const void *)pipe_kernel<8, true> : W == 16 ? (const void *)pipe_kernel<16, true> : nullptr;
+    return W == 8 ? (const void *)pipe_kernel<8, false> : W == 16 ? (const void *)pipe_kernel<16, false> : nullptr;
+}
+
+}  // namespace burg
+#else
 __global__ void pipe_fill_kernel(v4u *p, size_t n, int color)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1159,11 +1179,7 @@ __global__ void halo_probe_kernel(v4u *ring, unsigned bytes, int put_at, v4u put
 template <bool SWEEP>
 const void *kernel_of(int W)
 {
-    switch (W) {
-    case 8: return (const void *)pipe_kernel<8, SWEEP>;
-    case 16: return (const void *)pipe_kernel<16, SWEEP>;
-    default: break;
-    }
+    if (W <= 16) return pipe_narrow_fn(W, SWEEP);  // (the other translation unit)
     if constexpr (!SWEEP) {
         switch (W) {
         case 32: return (const void *)pipe_kernel<32, false>;
@@ -1302,3 +1318,4 @@ int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st)
 }
 
 }  // namespace burg
+#endif  // BURG_PIPE_NARROW_TU

@@ -25,6 +25,8 @@ SRC = os.path.join(ROOT, "finitedifference_amd", "csrc", "pipe.hip")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
          "-Wno-bitwise-instead-of-logical",
          "-mllvm", "-amdgpu-sched-strategy=max-ilp"]  # as the Makefile builds pipe.hip
+FLAGS_NARROW = FLAGS[:-2]
+SRC_NARROW = os.path.join(ROOT, "finitedifference_amd", "csrc", "pipe_narrow.hip")
 
 
 def kind(op):
@@ -95,9 +97,15 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "pipe_isa.json"))
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
+        # wide kernels: pipe.hip with max-ilp; narrow: pipe_narrow.hip with the
+        # default scheduler (as the Makefile builds them)
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "-c", SRC, "-o", os.path.join(d, "p.o"),
                         "-save-temps"], cwd=d, check=True, capture_output=True)
         asm = open(os.path.join(d, "pipe-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
+        subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS_NARROW, "-c", SRC_NARROW, "-o",
+                        os.path.join(d, "n.o"), "-save-temps"], cwd=d, check=True,
+                       capture_output=True)
+        asm += open(os.path.join(d, "pipe_narrow-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
     res = {"source": "tools/isa_count.py (hipcc -O3 --offload-arch=gfx950 -save-temps of pipe.hip)",
            "issue_model": "4 cycles per instruction + 12 per fp64 transcendental (one wave per SIMD)"}
     for W, sweep in ((256, False), (16, True), (16, False)):
@@ -105,7 +113,8 @@ def main():
         rr = [r[i:i + U] for r in runs(kernel_body(asm, W, sweep)) for i in range(0, len(r), U)]
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
-        names = {1: ["block"], 2: ["interior_block", "edge_block"],
+        names = {1: ["block"], 2: ["steady_edge_block", "edge_block"] if W <= 16 else
+                 ["interior_block", "edge_block"],
                  3: ["steady_block", "interior_block", "edge_block"],
                  4: ["steady_block", "interior_block", "steady_edge_block", "edge_block"]}[len(rr)]
         res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}>"] = {
