@@ -870,9 +870,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         MarchCell::chain<true>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
         // (ballots of the single compares, combined on the scalar unit: a
         // ballot of the combined lane predicate costs a select and a compare)
+        // (steady blocks cover full strips: every lane is a row)
         const unsigned long long bad =
-            __builtin_amdgcn_ballot_w64(!ok) &
-            (STEADY ? rowmask : __builtin_amdgcn_ballot_w64(valid) & rowmask);
+            STEADY ? __builtin_amdgcn_ballot_w64(!ok)
+                   : __builtin_amdgcn_ballot_w64(!ok) & __builtin_amdgcn_ballot_w64(valid) & rowmask;
         if (__builtin_expect(bad != 0, 0)) {
             MarchCell::chain<false>(p, rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok);
             ++ieee_n;
