@@ -565,7 +565,7 @@ def test_slab_wide_rows_two_processes_one_gpu(gpu, orc, tmp_path):
 
 @pytest.mark.parametrize("W,N,T,world", [(128, 1024, 12, 2), (256, 1024, 6, 2), (1024, 2048, 2, 2),
                                          (128, 768, 10, 3)])
-def test_slab_wide_tile_steady_blocks_two_processes_one_gpu(gpu, orc, tmp_path, W, N, T, world):
+def test_slab_wide_tile_steady_blocks_one_gpu(gpu, orc, tmp_path, W, N, T, world):
     """Slabs whose tiles run the steady / steady-edge blocks (W > 64) on the
     strips that write the halo ring -- the multi-GPU bench's tiling (W = 256
     at 4096 x 4096 per GPU).  The halo ring's row is the whole slab width, so
