@@ -713,6 +713,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // diagonal uwrap of the block (>= U: no wrap in the block)
     unsigned noffs = 0, noffs2 = 0;
     int uwrap = U;
+    // narrow steady-edge blocks: the north slot offsets as per-lane values
+    // (kOOB on every lane but a north-writing top lane: no scalar state, no
+    // branch), and the inlet term added at column 0 (0 off the inlet tile)
+    unsigned nv1 = kOOB, nv2 = kOOB;
+    double lb_se = 0.0;
     auto fetch = [&](auto edge_tag, int s) -> In {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
@@ -845,7 +850,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const double pu = x.x, pv = x.y;
             const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
             const double srcc = SWEEP ? in.src : co.y;
-            const double sl = (col0_tile && at0) ? srcc + lbu : srcc;
+            // (narrow steady edge: srcc + 0.0 is srcc exactly -- the source
+            // term is positive -- so both forms give the same bits)
+            const double sl = (!WIDE && STEADY) ? srcc + (at0 ? lb_se : 0.0)
+                                                : (col0_tile && at0) ? srcc + lbu : srcc;
             p.hx = hx;
             const double hu = 0.5 * pu;
             p.xfp = ax * (hu * pu);
@@ -934,9 +942,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, noffs, no);
                     noffs += ncol;
                 } else {
-                    const unsigned so = u < uwrap ? noffs + (unsigned)u * ncol
-                                                  : noffs2 + (unsigned)(u - uwrap) * ncol;
-                    st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, so, no);
+                    st_sys(nrs, (u < uwrap ? nv1 : nv2) + (unsigned)u * ncol, no);
                 }
             } else {
                 const unsigned off = (out_n & (c < ncol_real))
@@ -996,6 +1002,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             int se_qw = 0;
             bool se_in = false;
             if constexpr (decltype(tag)::value == 3) {
+                if constexpr (!WIDE) lb_se = col0_tile ? lb : 0.0;  // (no switch inside)
                 // the lane's column-0 and column-(W-1) cells in this block
                 const int c0 = (sb - lane) & (W - 1);
                 se_uw = (W - c0) & (W - 1);
@@ -1106,6 +1113,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
             noffs2 = nb + (unsigned)((a.qbase + (tt0 >> LW) + 1) & (kR - 1)) * nstep;
             uwrap = W - ct0;
+            if constexpr (!WIDE) {
+                // (nv2 + u ncol for u >= uwrap is noffs2 + (u - uwrap) ncol,
+                // modulo 2^32)
+                const bool tl = has_north & (lane == top);
+                nv1 = tl ? noffs : kOOB;
+                nv2 = tl ? noffs2 - (unsigned)uwrap * ncol : kOOB;
+            }
         }
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
             // (narrow-or-equal tiles, W <= 64: one block's lanes span several
