@@ -541,6 +541,13 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
 {
     BURG_TRACE("march launch");
     const bool pipe = c->eng_eff == BURG_ENGINE_PIPE;
+    // test hook (BURG_TEST_FAIL_DEVICE_HALO=1): a launch with a device-memory
+    // halo ring fails as a stalled halo wait would, without launching --
+    // exercises the bench's fall-back to the host rings (tools/gpu_round.sh)
+    if (const char *e = std::getenv("BURG_TEST_FAIL_DEVICE_HALO"))
+        if (std::strcmp(e, "1") == 0 && (c->halo_in_mode == 2 || c->halo_out_mode == 2))
+            return fail(BURG_EHIP, "pipe engine: a wait timed out (test hook "
+                                   "BURG_TEST_FAIL_DEVICE_HALO: device halo ring)");
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
         CHK(launch_pipe(pipe_args(c, L, origin, K), c->sp.W, c->stream));

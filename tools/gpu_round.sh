@@ -18,6 +18,10 @@ cat $O/bench.json
 # workgroups are resident together)
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rehearse-one-gpu --nx 2048 --rows-per-gpu 1024 --stream-w 128 --steps 5 --warmup 1 > $O/bench_rehearse_n2.json 2> $O/bench_rehearse.err || { tail -20 $O/bench_rehearse.err; exit 1; }
 cat $O/bench_rehearse_n2.json
+# the same with every device-ring launch failing (test hook): the bench must
+# fall back to the host rings on all ranks and still print its line
+BURG_TEST_FAIL_DEVICE_HALO=1 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 2 --rehearse-one-gpu --nx 2048 --rows-per-gpu 1024 --stream-w 128 --steps 5 --warmup 1 > $O/bench_rehearse_fallback.json 2> $O/bench_rehearse_fallback.err || { tail -20 $O/bench_rehearse_fallback.err; exit 1; }
+grep '"halo_fallback": "device' $O/bench_rehearse_fallback.json > /dev/null || { echo "no fall-back recorded"; exit 1; }
 timeout -k 10 300 python tools/snapio_probe.py 1024 100 /tmp/snapio > $O/snapio_1024.json 2> $O/snapio.err || { tail -20 $O/snapio.err; exit 1; }
 cat $O/snapio_1024.json
 echo ALLOK
