@@ -198,7 +198,7 @@ struct LspgArgs {
     const double *btT;   // basis, (npod, 2n), each plane transposed
     const double *r;     // residual R(w; wp) (2n)
     int npod;
-    const double *bk;    // basis blocked by 32-cell tiles (lspg_gram_blocked): [tile][k][4][32]
+    const double *bk;    // basis blocked by 32-cell tiles (lspg_gram_blocked): [tile][k][2][32][2]
 };
 int lspg_cols(int npod);
 size_t lspg_partial_count(int nx, int npod);

@@ -372,13 +372,14 @@ __global__ __launch_bounds__(kLB + FW * 64) void lspg_gram_ws_kernel(LspgArgs a,
                 const int r = (int)(ii / N), c = (int)(ii - (size_t)r * N);
                 const bool west = c > 0, south = r > 0;
                 const size_t iw = west ? ii - 1 : ii, is = south ? ii - N : ii;
-                // blocked basis: cell i, column k, array e (xu, xv, xuT, xvT) at
-                // ((i / 32 * npod + k) * 4 + e) * 32 + i % 32 -- one tile's values
+                // blocked basis: the (u, v) pair of cell i, column k, plane s
+                // (0 straight, 1 transposed) at ((i / 32 * npod + k) * 2 + s) *
+                // 64 + (i % 32) * 2 -- one 16-B load per pair; a tile's values
                 // for all columns are one contiguous run (few pages, full lines)
                 const size_t np = (size_t)a.npod;
-                const double *bi = a.bk + (ii / kMC) * np * 128 + (ii % kMC);
-                const double *bw = a.bk + (iw / kMC) * np * 128 + (iw % kMC);
-                const double *bs = a.bk + (is / kMC) * np * 128 + (is % kMC) + 64;
+                const double *bi = a.bk + (ii / kMC) * np * 128 + (ii % kMC) * 2;
+                const double *bw = a.bk + (iw / kMC) * np * 128 + (iw % kMC) * 2;
+                const double *bs = a.bk + (is / kMC) * np * 128 + (is % kMC) * 2 + 64;
                 const double *u = a.w, *v = a.w + n, *uT = a.wT, *vT = a.wT + n;
                 const double ui = u[ii], vi = v[ii], uW = u[iw], vW = v[iw];
                 const double uTi = uT[ii], vTi = vT[ii], uTS = uT[is], vTS = vT[is];
@@ -392,8 +393,12 @@ __global__ __launch_bounds__(kLB + FW * 64) void lspg_gram_ws_kernel(LspgArgs a,
                     for (int q = 0; q < CH; ++q) {
                         const int k = kg + KS * (q0 + q);
                         const size_t ko = (size_t)(k < a.npod ? k : a.npod - 1) * 128;  // valid column
-                        xl[q][0] = bi[ko], xl[q][1] = bi[ko + 32], xl[q][2] = bw[ko], xl[q][3] = bw[ko + 32];
-                        xl[q][4] = bi[ko + 64], xl[q][5] = bi[ko + 96], xl[q][6] = bs[ko], xl[q][7] = bs[ko + 32];
+                        const double2 pi = *(const double2 *)(bi + ko);
+                        const double2 pw = *(const double2 *)(bw + ko);
+                        const double2 pt = *(const double2 *)(bi + ko + 64);
+                        const double2 ps = *(const double2 *)(bs + ko);
+                        xl[q][0] = pi.x, xl[q][1] = pi.y, xl[q][2] = pw.x, xl[q][3] = pw.y;
+                        xl[q][4] = pt.x, xl[q][5] = pt.y, xl[q][6] = ps.x, xl[q][7] = ps.y;
                     }
 #pragma unroll
                     for (int q = 0; q < CH; ++q) {
@@ -479,9 +484,10 @@ __global__ __launch_bounds__(kLB + FW * 64) void lspg_gram_ws_kernel(LspgArgs a,
     }
 }
 
-// Blocked basis for the warp-specialised Gram kernel: bk[((t npod + k) 4 + e)
-// 32 + j] = array e (xu, xv, xuT, xvT) of basis column k at cell 32 t + j
-// (zero past the last cell).  Built once per LSPG run from bt / btT.
+// Blocked basis for the warp-specialised Gram kernel: bk[((t npod + k) 2 + s)
+// 64 + 2 j + e] = component e (u, v) of plane s (0: bt, 1: btT) of basis
+// column k at cell 32 t + j (zero past the last cell): each cell's (u, v)
+// pair is one 16-B load.  Built once per LSPG run from bt / btT.
 __global__ __launch_bounds__(kLB) void lspg_block_basis_kernel(const double *__restrict__ bt,
                                                                const double *__restrict__ btT,
                                                                size_t n, int npod,
@@ -491,13 +497,13 @@ __global__ __launch_bounds__(kLB) void lspg_block_basis_kernel(const double *__r
     const size_t total = ntiles * (size_t)npod * 128;
     const size_t m = 2 * n;
     for (size_t o = (size_t)blockIdx.x * kLB + threadIdx.x; o < total; o += (size_t)gridDim.x * kLB) {
-        const int j = (int)(o & 31), e = (int)((o >> 5) & 3);
+        const int e = (int)(o & 1), j = (int)((o >> 1) & 31), sp = (int)((o >> 6) & 1);
         const size_t tk = o >> 7;
         const size_t t = tk / npod, k = tk - t * npod;
         const size_t i = t * kMC + j;
         double x = 0.0;
         if (i < n) {
-            const double *src = (e < 2 ? bt : btT) + k * m + (e & 1) * n;
+            const double *src = (sp ? btT : bt) + k * m + (size_t)e * n;
             x = src[i];
         }
         bk[o] = x;
