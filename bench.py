@@ -12,16 +12,26 @@ exactly by the HIP march in ONE pipelined launch (burg_trajectory).
 --sweep N times the snapshot sweep over the first N training mu instead
 (burg_sweep; C/run_prom.py:59-71).
 
-Workload (BASELINE.json configs[2], the largest single-GPU config): 4096 x
-4096 cells per GPU, fp64.  dt = 0.05 * 1024 / nx: the CFL number of the
-1024^2 configuration (dt = 0.05 there, as run_fom.py).  With dt = 0.05 at
-4096^2 the reference scheme itself is unstable (dt > 2h: v < 0 at the
-boundary, NaN after 14 steps -- measured with the oracle),
-so a fixed dt would time NaN arithmetic.  N > 1: weak scaling by row slabs,
-rank k owning rows [4096k, 4096k + 4096) of a 4096 x 4096N grid (same cell
-size, same dt), the one-way halo streamed GPU-to-GPU during the launch
-(DESIGN.md section 7).  value = N * 4096^2 * T * K / (max over ranks of the
+Workload, by GPU count (defaults; --nx / --rows-per-gpu override):
+  N = 1: BASELINE.json configs[2] (the largest single-GPU config), 4096^2;
+  N = 2: 8192 x 4096 (8192 x 2048 per GPU: configs[3]'s slab, half its rows);
+  N = 4: BASELINE configs[3], 8192^2 (8192 x 2048 per GPU);
+  N = 8: BASELINE configs[4], 16384^2 (16384 x 2048 per GPU: SURVEY.md 8(d)'s
+         weak-scaling slab).
+fp64, dt = 0.05 * 1024 / nx: the CFL number of the 1024^2 configuration
+(dt = 0.05 there, as run_fom.py).  With dt = 0.05 at 4096^2 the reference
+scheme itself is unstable (dt > 2h: v < 0 at the boundary, NaN after 14 steps
+-- measured with the oracle), so a fixed dt would time
+NaN arithmetic.  N > 1: row slabs, rank k owning rows [k*rows, (k+1)*rows) of
+the nx x N*rows grid, the one-way halo streamed GPU-to-GPU during the launch
+(DESIGN.md section 7).  value = nx * N*rows * T * K / (max over ranks of the
 wall time of the K timed trajectories), inputs resident in HBM.
+After the timed region every run checks its own result (residual_check):
+the last step of a trajectory must solve the reference residual,
+||R(w_T; w_{T-1})|| / ||R(w_{T-1}; w_{T-1})|| < 1e-13 (C/hypernet2D.py:2512-2570),
+computed slab by slab with the south halo rows sent by the rank below
+(burg_slab_residual + torch.distributed send/recv); the bench exits non-zero
+if it fails.
 
 Extra JSON objects: roofline (the march kernel: algorithmic 32 B per
 cell-update = read the previous state u, v + write the new state u, v,
@@ -65,12 +75,17 @@ def parse():
                          "(get_snapshot_params); 1 = one trajectory at mu=(5.19, 0.026)")
     ap.add_argument("--time-steps", type=int, default=500,
                     help="implicit steps per trajectory (run_fom.py: 500)")
-    ap.add_argument("--nx", type=int, default=4096)
+    ap.add_argument("--nx", type=int, default=None,
+                    help="row length (default by GPU count: 4096, 8192, 8192, 16384 for N = 1, 2, "
+                         "4, 8)")
     ap.add_argument("--dt", type=float, default=None,
                     help="time step (default 0.05 * 1024 / nx: the 1024^2 config's CFL)")
     ap.add_argument("--no-1024", action="store_true",
                     help="skip the secondary BASELINE configs[1] line (1024^2 9-mu sweep)")
-    ap.add_argument("--rows-per-gpu", type=int, default=None)
+    ap.add_argument("--rows-per-gpu", type=int, default=None,
+                    help="rows per GPU (default: nx at N = 1, 2048 at N > 1)")
+    ap.add_argument("--no-residual-check", action="store_true",
+                    help="skip the post-run residual check of the last step")
     ap.add_argument("--engine", default="pipe", choices=["pipe", "stream"])
     ap.add_argument("--stream-w", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -103,6 +118,28 @@ def host_threads():
     n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     omp = os.environ.get("OMP_NUM_THREADS")
     return max(1, min(n, int(omp))) if omp and omp.isdigit() else n
+
+
+# BASELINE.json configs by (nx, ny, GPUs)
+BASELINE_CONFIGS = {(1024, 1024, 1): 1, (4096, 4096, 1): 2, (8192, 8192, 4): 3,
+                    (16384, 16384, 8): 4}
+DEFAULT_SHAPES = {1: (4096, 4096), 2: (8192, 2048), 4: (8192, 2048), 8: (16384, 2048)}
+
+
+def default_shape(world, nx=None, rows=None):
+    """(nx, rows per GPU) of the bench by GPU count (module docstring)."""
+    dnx, drows = DEFAULT_SHAPES.get(world, (8192, 2048))
+    if nx is None:
+        nx = dnx
+        rows = rows or drows
+    else:
+        rows = rows or (nx if world == 1 else 2048)
+    return nx, rows
+
+
+def workload_label(nx, ny, world):
+    k = BASELINE_CONFIGS.get((nx, ny, world))
+    return f"BASELINE configs[{k}]" if k is not None else "not a BASELINE config"
 
 
 def cpu_baseline(nx, dt, seconds):
@@ -138,6 +175,21 @@ def cpu_baseline(nx, dt, seconds):
     eln = time.perf_counter() - t0
     return {"value": round(march, 3), "unit": "Mcell-updates/s", "cores": int(used),
             "kind": "port", "nproc": os.cpu_count(),
+            "threads_note": ("threads = this process's CPU share: the GPU pool gives a one-GPU "
+                             "box 16 host threads (OMP_NUM_THREADS=16, affinity capped), while "
+                             "nproc counts the whole machine"),
+            "reference_measured": {
+                "what": "the reference itself (C/run_fom.py -> inviscid_burgers_implicit2D, "
+                        "NumPy/SciPy SuperLU, 1 core); it cannot run on the GPU box and is "
+                        "infeasible at this grid (SuperLU: 183 s for ONE step at 1024^2, OOM "
+                        "at 4096^2)",
+                "coarse_250": {"value": 0.0501, "unit": "Mcell-updates/s", "cores": 1,
+                               "source": "SURVEY.md section 6 / 8(d): 250^2 x 500 steps in "
+                                         "623.3 s, build container (Xeon, "
+                                         "OPENBLAS_NUM_THREADS=1)"},
+                "fine_750_sherlock": {"value": 0.0116, "unit": "Mcell-updates/s", "cores": 1,
+                                      "source": "F/output_55034725.log:1005 (the author's "
+                                                "750^2 x 500 run on Sherlock), BASELINE.md"}},
             "sample": f"oracle march (orc_march_sweep, OpenMP) on {nx}x{nx}, dt={dt:g}: {len(mus)} "
                       f"trajectories (training mu) x {steps} steps from w0=1, one per thread, "
                       f"{el:.1f} s on {used} threads",
@@ -313,8 +365,7 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (use torchrun for N > 1)",
               file=sys.stderr)
         sys.exit(2)
-    nx = args.nx
-    rows = args.rows_per_gpu or nx
+    nx, rows = default_shape(world, args.nx, args.rows_per_gpu)
     ny = rows * world
     T = args.time_steps
     dt = args.dt if args.dt is not None else DT * 1024.0 / nx
@@ -357,10 +408,22 @@ def main():
         torch.cuda.synchronize()
 
     def measure(c):
+        """Warm-up and timed trajectories.  Every rank runs the same sequence
+        of collectives whatever happens: a step that raises records the error
+        and the rank skips its remaining launches (its neighbours' bounded halo
+        waits then give up too), so the agreement below always pairs up."""
+        err = []
+
         def one_step():
-            if nmu == 1:
-                return c.trajectory(T)
-            return c.sweep(mus, T, keep_snaps=False)[1]
+            if err:
+                return None
+            try:
+                if nmu == 1:
+                    return c.trajectory(T)
+                return c.sweep(mus, T, keep_snaps=False)[1]
+            except BurgersError as e:
+                err.append(e)
+                return None
         for _ in range(args.warmup):
             barrier()
             one_step()
@@ -371,43 +434,51 @@ def main():
         s = None
         for _ in range(args.steps):
             s = one_step()
-            kern += s["loop_ms"]
-            nl += max(1, s["stream_launches"])
+            if s is not None:
+                kern += s["loop_ms"]
+                nl += max(1, s["stream_launches"])
         barrier()
-        return time.perf_counter() - t0, kern, nl, s
+        return (time.perf_counter() - t0, kern, nl, s), (err[0] if err else None)
 
+    def agree(c, e):
+        """0: every rank ok; 1: some rank's device halo ring stalled (a wait
+        timed out with a device ring on one of its boundaries) -- fall back to
+        the host rings; 2: any other failure -- re-raise everywhere."""
+        code = 0
+        if e is not None:
+            hin, hout = c.halo_modes()
+            code = 1 if ("wait timed out" in str(e) and 2 in (hin, hout)) else 2
+        if world == 1:
+            return code
+        t = torch.tensor([code], dtype=torch.int32, device="cpu" if rehearse else "cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t.item())
+
+    from finitedifference_amd._lib import BurgersError
     ctx = setup()
     halo_fallback = None
-    if world == 1:
-        elapsed, kern_ms, launches, st = measure(ctx)
-    else:
-        # a device-memory halo ring that passed its self-test but stalls under
-        # the real protocol makes every rank's bounded waits give up: all
-        # ranks then agree to measure again on the pinned host rings
-        from finitedifference_amd._lib import BurgersError
-        err = None
-        try:
-            res = measure(ctx)
-        except BurgersError as e:
-            err, res = str(e), None
-        ok = torch.tensor([0 if err else 1], dtype=torch.int32,
-                          device="cpu" if rehearse else "cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 0:
-            if os.environ.get("BURG_HALO") == "host":
-                raise RuntimeError(f"rank {rank}: multi-GPU run failed on the host halo rings: {err}")
-            halo_fallback = f"device halo ring failed ({err or 'on another rank'}); host rings"
-            print(f"bench.py rank {rank}: {halo_fallback}", file=sys.stderr, flush=True)
-            ctx.close()
-            os.environ["BURG_HALO"] = "host"
-            os.environ.pop("BURG_TEST_FAIL_DEVICE_HALO", None)
-            ctx = setup()
-            res = measure(ctx)
-        elapsed, kern_ms, launches, st = res
+    res, err = measure(ctx)
+    code = agree(ctx, err)
+    if code == 1 and os.environ.get("BURG_HALO") != "host":
+        halo_fallback = f"device halo ring failed ({err or 'on another rank'}); host rings"
+        print(f"bench.py rank {rank}: {halo_fallback}", file=sys.stderr, flush=True)
+        ctx.close()
+        os.environ["BURG_HALO"] = "host"
+        os.environ.pop("BURG_TEST_FAIL_DEVICE_HALO", None)
+        ctx = setup()
+        res, err = measure(ctx)
+        code = agree(ctx, err)
+    if code:
+        raise RuntimeError(f"rank {rank}: the timed run failed ({err or 'on another rank'})")
+    elapsed, kern_ms, launches, st = res
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    check = None
+    if not args.no_residual_check:
+        check = residual_check(ctx, T, dist if world > 1 else None,
+                               None if rehearse or world == 1 else dev)
     cells = nx * ny  # whole job
     value = cells * T * nmu * args.steps / elapsed / 1e6
 
@@ -454,13 +525,16 @@ def main():
                 "workload": f"implicit 2D inviscid Burgers FOM (run_fom time loop), "
                             f"{nx}x{rows} cells per GPU (grid {nx}x{ny}), fp64, "
                             f"{T} implicit steps per trajectory, {nmu} trajectories (mu) "
-                            f"per step, exact march on MI355X (BASELINE configs[2] at N=1)",
+                            f"per step, exact march on {world}x MI355X "
+                            f"({workload_label(nx, ny, world)})",
+                "baseline_config": BASELINE_CONFIGS.get((nx, ny, world)),
                 "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T, "dt": dt,
                 "trajectories_per_step": nmu,
                 "parallelism": f"row-slab x{world}",
                 "halo_ring": halo,
                 "halo_fallback": halo_fallback,
             },
+            "residual_check": check,
             "engine": {"name": eng, "tile_w": st["stream_w"], "tiles": st["stream_tiles"],
                        "blocked_diagonals": st["slow_diagonals"],
                        "spin_polls": st["stall_spins"], "ieee_diagonals": st["ieee_diagonals"],
@@ -497,6 +571,45 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    if check is not None and not check["ok"]:
+        print(f"bench.py: residual check failed: {check}", file=sys.stderr, flush=True)
+        sys.exit(3)
+
+
+RESIDUAL_TOL = 1e-13
+
+
+def residual_check(ctx, T, dist=None, device=None):
+    """The run checks its own result: w_{T-1} and w_T of the bench's
+    trajectory (burg_trajectory from w0 at mu = (5.19, 0.026)) are taken from
+    two more launches, and the last step must solve the reference residual
+    (C/hypernet2D.py:2512-2570): ||R(w_T; w_{T-1})|| / ||R(w_{T-1}; w_{T-1})||
+    < RESIDUAL_TOL, norms over the whole grid (slab residuals with the halo
+    rows from the rank below, summed over ranks).  Also the largest per-slab
+    ratio (max over ranks)."""
+    from finitedifference_amd.dist import slab_residual_norms
+    if T >= 2:
+        ctx.trajectory(T - 1)
+        wpm = ctx.download()
+    else:
+        wpm = np.ones(ctx.m)  # the uploaded w0
+    ctx.trajectory(T)
+    wT = ctx.download()
+    n1, s1 = slab_residual_norms(ctx, wT, wpm, dist, device)
+    n0, s0 = slab_residual_norms(ctx, wpm, wpm, dist, device)
+    rel = n1 / n0 if n0 > 0 else float("inf")
+    srel = s1 / s0 if s0 > 0 else float("inf")
+    if dist is not None:
+        import torch
+        t = torch.tensor([srel], dtype=torch.float64,
+                         device="cpu" if device is None else torch.device("cuda", device))
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        srel = float(t.item())
+    return {"what": "||R(w_T; w_(T-1))|| / ||R(w_(T-1); w_(T-1))|| of the last step, reference "
+                    "residual res2D_alt (C/hypernet2D.py:2512-2570), slab by slab with the halo "
+                    "rows from the rank below",
+            "rel": rel, "max_over_ranks_slab_rel": srel, "norm_R_T": n1, "norm_R_T-1": n0,
+            "tol": RESIDUAL_TOL, "ok": bool(rel < RESIDUAL_TOL and srel < RESIDUAL_TOL)}
 
 
 def config2_1024(pmc_file, isa_file=None, steps=3):

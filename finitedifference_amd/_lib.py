@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -24,7 +24,7 @@ ENGINES = {"stream": 0, "tiles": 1, "pipe": 2}
 EXPORTS = (
     "burg_abi_version", "burg_last_error", "burg_ctx_create", "burg_ctx_create_slab",
     "burg_slab_connect", "burg_slab_verify", "burg_slab_halo_note", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
-    "burg_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
+    "burg_residual", "burg_slab_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
     "burg_reserve_trajectory",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
@@ -121,6 +121,7 @@ def load(path=None):
             "burg_set_options": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                                 ctypes.c_double, ctypes.c_int]),
             "burg_residual": (ctypes.c_int, [_VP, _D, _D, _D, _D]),
+            "burg_slab_residual": (ctypes.c_int, [_VP, _D, _D, _D, _D, _D, _D]),
             "burg_jvp": (ctypes.c_int, [_VP, _D, _D, _D]),
             "burg_block_solve": (ctypes.c_int, [_VP, _D, _D, _D]),
             "burg_run": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, ctypes.c_int,

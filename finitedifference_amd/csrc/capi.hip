@@ -159,6 +159,7 @@ struct burg_ctx {
     int halo_in_mode = 0, halo_out_mode = 0;             // 0 unknown, 1 host, 2 device
     size_t halo_bytes = 0;
     bool halo_connected = false;
+    bool slab_failed = false;        // a launch failed: refuse further launches (BURG_ESTATE)
     bool halo_out_resolved = false;  // producer: took the consumer's verdict (first launch)
     std::string halo_note;           // why a device ring was not used
 
@@ -343,6 +344,7 @@ void stream_free(burg_ctx *c)
     dfree(c->d_err);
     dfree(c->d_sstats);
     c->ring_entries = 0;
+    c->ring_maxed = false;
     c->sp_ready = c->colc_ready = false;
 }
 
@@ -470,6 +472,7 @@ int ensure_ring(burg_ctx *c, long long L)
     if (need <= c->ring_entries) return 0;
     dfree(c->d_ring);
     c->ring_entries = 0;
+    c->ring_maxed = false;  // a ring sized for L, not to the memory limit
     if (int e = dalloc(&c->d_ring, need)) return e;
     c->ring_entries = need;
     return 0;
@@ -541,13 +544,19 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
 {
     BURG_TRACE("march launch");
     const bool pipe = c->eng_eff == BURG_ENGINE_PIPE;
+    if (c->slab_failed)
+        return fail(BURG_ESTATE, "a launch of this slab context failed earlier: its halo rings hold "
+                                 "stale step colours, so every rank must destroy and recreate its "
+                                 "context");
     // test hook (BURG_TEST_FAIL_DEVICE_HALO=1): a launch with a device-memory
     // halo ring fails as a stalled halo wait would, without launching --
     // exercises the bench's fall-back to the host rings (tools/gpu_round.sh)
     if (const char *e = std::getenv("BURG_TEST_FAIL_DEVICE_HALO"))
-        if (std::strcmp(e, "1") == 0 && (c->halo_in_mode == 2 || c->halo_out_mode == 2))
+        if (std::strcmp(e, "1") == 0 && (c->halo_in_mode == 2 || c->halo_out_mode == 2)) {
+            c->slab_failed = true;
             return fail(BURG_EHIP, "pipe engine: a wait timed out (test hook "
                                    "BURG_TEST_FAIL_DEVICE_HALO: device halo ring)");
+        }
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
         CHK(launch_pipe(pipe_args(c, L, origin, K), c->sp.W, c->stream));
@@ -562,6 +571,9 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
     unsigned err[4] = {0, 0, 0, 0};
     HIPCHK(hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
     if (err[0]) {
+        // a slab's halo rings (shared with its neighbours) cannot be reset by
+        // one rank alone: the context refuses further launches
+        if (c->world > 1) c->slab_failed = true;
         // leave the mailboxes clean for the next launch
         (void)hipMemsetAsync(c->d_err, 0, sizeof err, c->stream);
         if (pipe) {
@@ -699,7 +711,12 @@ int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_o
     const int W = c->sp.W;
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     long long C = std::min(num_steps, stream_max_steps(c));
+    if (const char *e = std::getenv("BURG_STREAM_CHUNK")) {  // test knob: force chunking
+        const long long v = std::atoll(e);
+        if (v > 0) C = std::min(C, v);
+    }
     const long long have_L = (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave));
+    bool maxed = false;
     if (C * W + W + 96 > have_L && !(c->ring_maxed && have_L >= 2 * W + 96)) {
         // need a (bigger) ring: size it against free memory
         dfree(c->d_ring);
@@ -708,14 +725,16 @@ int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_o
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
         const long long Lmax = (long long)(freeb / 100 * 85 / per_entry);
         const long long Cmem = (Lmax - W - 96) / W;
-        c->ring_maxed = Cmem < C;
+        maxed = Cmem < C;
         C = std::min<long long>(C, Cmem);
         if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
     } else {
         C = std::min<long long>(C, (have_L - W - 96) / W);
+        maxed = c->ring_maxed;
     }
     const long long L = C * W + W + 96;
     if (int e = ensure_ring(c, L)) return e;
+    c->ring_maxed = maxed;
     *C_out = C;
     *L_out = L;
     return 0;
@@ -787,6 +806,7 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
     if ((size_t)c->sp.ntiles * (size_t)L * kWave > c->ring_entries) {  // else reuse the ring
         dfree(c->d_ring);
         c->ring_entries = 0;
+        c->ring_maxed = false;  // sized for this run, not to the memory limit
         if (int e = ensure_ring(c, L)) return e;
     }
 
@@ -1336,6 +1356,43 @@ int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, dou
     HIPCHK(hipMemcpyAsync(r, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (norm) *norm = nrm;
+    return BURG_OK;
+}
+
+int burg_slab_residual(burg_ctx *c, const double *w, const double *wp, const double *halo_w,
+                       const double *halo_wp, double *r, double *sumsq)
+{
+    BURG_TRACE("burg_slab_residual");
+    if (int e = check_ready(c)) return e;
+    if (!w || !wp || !r) return fail(BURG_EINVAL, "null array");
+    if ((halo_w == nullptr) != (halo_wp == nullptr))
+        return fail(BURG_EINVAL, "halo_w and halo_wp must both be given or both be NULL");
+    if (halo_w && c->row0 == 0)
+        return fail(BURG_EINVAL, "the bottom slab (row 0) has no south halo row");
+    if (!halo_w && c->row0 > 0)
+        return fail(BURG_EINVAL, "a slab above row 0 needs the south halo rows (rows %d of w, wp)",
+                    c->row0 - 1);
+    if (int e = ensure_scratch(c)) return e;
+    const size_t bytes = c->m() * sizeof(double), hb = 2 * (size_t)c->nx * sizeof(double);
+    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->d_d, wp, bytes, hipMemcpyHostToDevice, c->stream));
+    double *d_halo = nullptr;
+    if (halo_w) {
+        if (int e = dalloc(&d_halo, 4 * (size_t)c->nx)) return e;
+        HIPCHK(hipMemcpyAsync(d_halo, halo_w, hb, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(d_halo + 2 * c->nx, halo_wp, hb, hipMemcpyHostToDevice, c->stream));
+    }
+    int rc = launch_residual(c->cf, c->d_x, c->d_d, c->d_r, c->d_partials, c->d_sumsq, d_halo,
+                             d_halo ? d_halo + 2 * c->nx : nullptr, c->stream);
+    double s = 0.0;
+    if (rc == 0 &&
+        (hipMemcpyAsync(r, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipMemcpyAsync(&s, c->d_sumsq, sizeof s, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+         hipStreamSynchronize(c->stream) != hipSuccess))
+        rc = -3;
+    dfree(d_halo);
+    if (rc) return fail(BURG_EHIP, "slab residual failed: %s", hipGetErrorString(hipGetLastError()));
+    if (sumsq) *sumsq = s;
     return BURG_OK;
 }
 

@@ -90,3 +90,63 @@ def make_slab_context(nx, ny, rank=0, world=1, device=0, dist=None, halo_name=No
     ctx.verify()
     dist.barrier()
     return ctx
+
+
+def top_row(w, nx, rows):
+    """[u row | v row] of a slab state's top row (the next slab's south halo)."""
+    w = np.asarray(w, dtype=np.float64).reshape(2, rows, nx)
+    return np.ascontiguousarray(w[:, rows - 1, :]).ravel()
+
+
+def exchange_halo_rows(rows_up, nx, rank, world, dist, device=None):
+    """One-way halo exchange of the row-slab decomposition: rank k sends
+    `rows_up` (a float64 array, e.g. the top rows of w and wp) to rank k+1
+    and receives rank k-1's (None on rank 0).  torch.distributed send/recv
+    (RCCL over xGMI with CUDA tensors when `device` is given, gloo on CPU
+    tensors otherwise) -- the exchange step of SURVEY.md section 8(e)."""
+    import torch
+    dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
+    rows_up = np.ascontiguousarray(rows_up, dtype=np.float64)
+    got = None
+    send = None
+    if rank + 1 < world:
+        send = torch.from_numpy(rows_up).to(dev)
+    if rank > 0:
+        got = torch.empty(rows_up.size, dtype=torch.float64, device=dev)
+    # even ranks send first, odd ranks receive first: no rank waits on a
+    # peer that is itself blocked in a send
+    if rank % 2 == 0:
+        if send is not None:
+            dist.send(send, dst=rank + 1)
+        if got is not None:
+            dist.recv(got, src=rank - 1)
+    else:
+        if got is not None:
+            dist.recv(got, src=rank - 1)
+        if send is not None:
+            dist.send(send, dst=rank + 1)
+    return None if got is None else got.cpu().numpy()
+
+
+def slab_residual_norms(ctx, w, wp, dist=None, device=None):
+    """Global ||R(w; wp)|| of a row-slab decomposition, every rank passing its
+    own slab rows of w and wp: the south halo rows come from the rank below
+    (exchange_halo_rows), each rank's sum of squares from burg_slab_residual,
+    summed over ranks (all_reduce).  Returns (global norm, this slab's norm).
+    Each slab's residual entries equal the single-domain residual's
+    (C/hypernet2D.py:2512-2570) bit for bit."""
+    nx, rows, rank, world = ctx.nx, ctx.ny, ctx.rank, ctx.world
+    if world == 1:
+        _, ss = ctx.slab_residual(w, wp)
+        return float(np.sqrt(ss)), float(np.sqrt(ss))
+    up = np.concatenate((top_row(w, nx, rows), top_row(wp, nx, rows)))
+    got = exchange_halo_rows(up, nx, rank, world, dist, device)
+    if got is None:
+        _, ss = ctx.slab_residual(w, wp)
+    else:
+        _, ss = ctx.slab_residual(w, wp, got[:2 * nx], got[2 * nx:])
+    import torch
+    dev = torch.device("cuda", device) if device is not None else torch.device("cpu")
+    t = torch.tensor([ss], dtype=torch.float64, device=dev)
+    dist.all_reduce(t)
+    return float(np.sqrt(t.item())), float(np.sqrt(ss))

@@ -395,7 +395,8 @@ def _commit_cache(tmp, fn, mm):
 
 
 def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="param_snaps",
-                          stream=False, mmap=False, direct=False, **solver_kw):
+                          stream=False, mmap=False, direct=False, recompute_short=False,
+                          **solver_kw):
     """Load cached snapshots for mu, or compute and cache them
     (C/hypernet2D.py:3111-3145; same file names and .npy format, so caches
     are interchangeable with the reference's).  solver_kw go to
@@ -414,7 +415,11 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
     the whole file.  direct=True (march solver): the library writes the cache
     file itself (burg_run_npy: the trajectory stays in HBM, row blocks of the
     C-order matrix go through two pinned buffers to a writer thread), then
-    the file is loaded (mmap=True: mapped)."""
+    the file is loaded (mmap=True: mapped).
+
+    A cache file with fewer columns than asked for is returned as it is,
+    truncated to what it holds (the reference's np.load(fn)[:, :num_steps+1]);
+    recompute_short=True recomputes it instead and overwrites the file."""
     if not os.path.exists(snap_folder):
         os.makedirs(snap_folder)
     every = int(solver_kw.get("snap_every", 1))
@@ -425,7 +430,7 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
                                suffix=".npy" if every == 1 else f"+every{every}.npy")
     if snap_fn in get_saved_params(snap_folder=snap_folder):
         cached = np.load(snap_fn, mmap_mode="r")
-        if cached.shape[1] >= ncols:
+        if cached.shape[1] >= ncols or not recompute_short:
             print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
             return cached[:, :ncols] if mmap else np.array(cached[:, :ncols])
         print(f"Saved snaps for mu1={mu[0]}, mu2={mu[1]} hold {cached.shape[1]} of the "

@@ -125,6 +125,24 @@ class FOMContext:
                                          ctypes.byref(nrm)))
         return r, nrm.value
 
+    def slab_residual(self, w, wp, halo_w=None, halo_wp=None):
+        """This slab's rows of R(w; wp) (burg_slab_residual): w, wp are the
+        slab's rows; halo_w / halo_wp = [u row | v row] of the global row just
+        below the slab (None on the bottom slab).  Returns (r, sum of squares
+        of r)."""
+        w, wp = self._vec(w, "w"), self._vec(wp, "wp")
+        hw = hwp = None
+        if halo_w is not None or halo_wp is not None:
+            hw = np.ascontiguousarray(np.asarray(halo_w, dtype=np.float64).ravel())
+            hwp = np.ascontiguousarray(np.asarray(halo_wp, dtype=np.float64).ravel())
+            if hw.size != 2 * self.nx or hwp.size != 2 * self.nx:
+                raise ValueError(f"halo rows need 2*nx = {2 * self.nx} entries")
+        r = np.empty(self.m)
+        ss = ctypes.c_double()
+        _lib.check(self._L.burg_slab_residual(self._h, _lib.dptr(w), _lib.dptr(wp), _lib.dptr(hw),
+                                              _lib.dptr(hwp), _lib.dptr(r), ctypes.byref(ss)))
+        return r, ss.value
+
     def jvp(self, w, x):
         w, x = self._vec(w, "w"), self._vec(x, "x")
         y = np.empty(self.m)

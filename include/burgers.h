@@ -51,14 +51,15 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 11
+#define BURG_ABI_VERSION 12
 
 enum burg_status {
     BURG_OK = 0,
     BURG_EINVAL = -1,   /* bad argument (null pointer, size, option) */
     BURG_ESHAPE = -2,   /* grid shape not supported (e.g. nx != ny in strict mode) */
     BURG_EHIP = -3,     /* HIP runtime error */
-    BURG_EHALO = -4,    /* multi-GPU halo ring (shared host memory) error */
+    BURG_EHALO = -4,    /* multi-GPU halo ring error (rendezvous object, device ring over IPC
+                           or its pinned host fallback) */
     BURG_ENOMEM = -5,   /* device or pinned-host allocation failed */
     BURG_ENOCONV = -6,  /* solver hit its iteration cap (result still returned) */
     BURG_ENAN = -7,     /* non-finite residual or state */
@@ -110,8 +111,10 @@ enum burg_engine {
                                 by the compute waves (any tile width) */
     BURG_ENGINE_TILES = 1,   /* one step at a time: block-Jacobi tile passes (burg_set_options) */
     BURG_ENGINE_PIPE = 2     /* default: the streaming march with LDS edges inside a workgroup
-                                and a comm wave per workgroup (tile width 8/16; falls back to
-                                STREAM on one GPU when the grid needs wider tiles) */
+                                and a comm wave per workgroup; narrow tiles (W = 8, 16) keep the
+                                previous step in LDS, wide tiles (W = 32 ... 1024) stream it back
+                                from the HBM ring through a loader wave; falls back to STREAM on
+                                one GPU only when no width up to 1024 keeps every tile resident */
 };
 
 int burg_abi_version(void);
@@ -184,6 +187,18 @@ int burg_set_engine(burg_ctx *ctx, int engine, int stream_w, int tiles_target);
 int burg_residual(burg_ctx *ctx, const double *w, const double *wp, double *r,
                   double *norm_out);
 int burg_jvp(burg_ctx *ctx, const double *w, const double *x, double *y);
+/* The residual of a slab context's rows (inviscid_burgers_res2D_alt,
+ * C/hypernet2D.py:2512-2570, restricted to global rows [row0, row0+nrows)):
+ * w, wp are this slab's rows (2*nx*nrows, as burg_run's w0); the south
+ * neighbour terms of the slab's first row come from halo_w / halo_wp =
+ * [u row | v row] (2*nx doubles) of global row row0-1 of w and wp (both NULL
+ * on the bottom slab, required above it).  r: 2*nx*nrows; sumsq (may be
+ * NULL): the sum of squares of r (the caller sums over ranks for ||R||).
+ * Each entry equals burg_residual's on the whole grid bit for bit; the halo
+ * rows come from the rank below (finitedifference_amd/dist.py, a
+ * torch.distributed send/recv).  Any context (world == 1: halos NULL). */
+int burg_slab_residual(burg_ctx *ctx, const double *w, const double *wp, const double *halo_w,
+                       const double *halo_wp, double *r, double *sumsq);
 int burg_block_solve(burg_ctx *ctx, const double *w, const double *rhs, double *delta);
 
 /* Time loop (inviscid_burgers_implicit2D).  w0: this context's rows of the

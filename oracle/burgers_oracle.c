@@ -38,7 +38,9 @@
  * the build's own exact solver for the same implicit step
  * and is restated here op-for-op as the bitwise checker of the HIP march.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <math.h>
+#include <sched.h>
 #ifdef _OPENMP
 #include <omp.h>
 #endif
@@ -308,6 +310,106 @@ int orc_march_sweep(int nx, int ny, const double *inv_dx, const double *inv_dy,
         free(a);
         free(b);
     }
+    return used;
+}
+
+/* ------------------------------------------------------------------------ */
+/* The same march, rows pipelined over OpenMP threads (test support: the
+ * checker for whole trajectories at the bench's sizes, 4096^2 x 500 steps,
+ * where the serial step takes minutes).  Not a new algorithm: every cell runs
+ * the loop body of orc_march_step with the same operands in the same order,
+ * so the result is orc_march_step's bit for bit.  Row r's thread marches
+ * columns [c0, c0 + 64) once row r-1 has published that it is past c0 + 64;
+ * the north outflows live in one in-place array exactly as in the serial
+ * version (row r overwrites yh[c] after reading it, row r+1 reads it after
+ * row r's publish).  prog[r] = s*(nx+1) + columns done in step s (monotone,
+ * never reset).  out: (num_steps/snap_every + 1) x 2n step-major (state after
+ * j*snap_every steps in row j).  Returns the threads used.                   */
+#define ORC_PAR_BLK 64
+int orc_march_traj_par(int nx, int ny, const double *inv_dx, const double *inv_dy,
+                       const double *src, const double *lbc, double dt, const double *w0,
+                       int num_steps, int snap_every, double *out, int threads)
+{
+    const size_t n = (size_t)nx * ny, m = 2 * n;
+    const double a = 0.5 * dt;
+    double *A = (double *)malloc(m * sizeof(double));
+    double *B = (double *)malloc(m * sizeof(double));
+    double *yh = (double *)calloc((size_t)nx, sizeof(double));
+    double *yg = (double *)calloc((size_t)nx, sizeof(double));
+    int64_t *prog = (int64_t *)calloc((size_t)ny, sizeof(int64_t));
+    memcpy(A, w0, m * sizeof(double));
+    memcpy(out, w0, m * sizeof(double));
+    int used = 1;
+#pragma omp parallel num_threads(threads)
+    {
+        int t = 0, T = 1;
+#ifdef _OPENMP
+        t = omp_get_thread_num();
+        T = omp_get_num_threads();
+#endif
+        if (t == 0) used = T;
+        for (int s = 0; s < num_steps; ++s) {
+            const double *up = (s & 1) ? B : A, *vp = up + n;
+            double *u = (s & 1) ? A : B, *v = u + n;
+            const int keep = (s + 1) % snap_every == 0;
+            double *o = out + (size_t)((s + 1) / snap_every) * m;
+            const int64_t base = (int64_t)s * (nx + 1);
+            for (int r = t; r < ny; r += T) {
+                const double ay = a * inv_dy[r];
+                const double hy = 0.5 * ay;
+                double xfw = 0.0, xhw = 0.0;
+                for (int c0 = 0; c0 < nx; c0 += ORC_PAR_BLK) {
+                    const int c1 = c0 + ORC_PAR_BLK < nx ? c0 + ORC_PAR_BLK : nx;
+                    if (r > 0) {
+                        unsigned spins = 0;
+                        while (__atomic_load_n(&prog[r - 1], __ATOMIC_ACQUIRE) < base + c1)
+                            if (++spins > 4096u) {
+                                sched_yield();
+                                spins = 0;
+                            }
+                    }
+                    for (int c = c0; c < c1; ++c) {
+                        const size_t i = IDX(r, c, nx);
+                        const double ax = a * inv_dx[c];
+                        const double hx = 0.5 * ax;
+                        const double sl = c == 0 ? src[0] + lbc[r] : src[c];
+                        const double pu = up[i], pv = vp[i];
+                        const double hu = 0.5 * pu;
+                        const double xfp = ax * (hu * pu);
+                        const double xhp = ax * (hu * pv);
+                        const double yhp = ay * (hu * pv);
+                        const double ygp = ay * ((0.5 * pv) * pv);
+                        const double bu = ((pu - xfp) - yhp) + sl;
+                        const double bv = (pv - ygp) - xhp;
+                        const double yin = r == 0 ? 0.0 : yh[c], gin = r == 0 ? 0.0 : yg[c];
+                        const double cu = (bu + xfw) + yin;
+                        const double cv = (bv + gin) + xhw;
+                        const double mm = fma(hx, cu, hy * cv);
+                        const double sq = 0.5 + sqrt(0.25 + mm);
+                        const double nu = cu / sq, nv = cv / sq;
+                        const double hxu = hx * nu;
+                        xfw = fma(hxu, nu, xfp);
+                        xhw = fma(hxu, nv, xhp);
+                        yh[c] = fma(hy * nu, nv, yhp);
+                        yg[c] = fma(hy * nv, nv, ygp);
+                        u[i] = nu;
+                        v[i] = nv;
+                    }
+                    __atomic_store_n(&prog[r], base + c1, __ATOMIC_RELEASE);
+                }
+                if (keep) {
+                    memcpy(o + IDX(r, 0, nx), u + IDX(r, 0, nx), (size_t)nx * sizeof(double));
+                    memcpy(o + n + IDX(r, 0, nx), v + IDX(r, 0, nx), (size_t)nx * sizeof(double));
+                }
+            }
+#pragma omp barrier
+        }
+    }
+    free(A);
+    free(B);
+    free(yh);
+    free(yg);
+    free(prog);
     return used;
 }
 

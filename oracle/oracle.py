@@ -131,6 +131,20 @@ class Problem:
                                      _p(np.ascontiguousarray(w0, dtype=np.float64)), len(mus),
                                      int(num_steps), int(threads))
 
+    def march_traj(self, w0, num_steps, snap_every=1, threads=None):
+        """orc_march_step's trajectory, rows pipelined over OpenMP threads
+        (orc_march_traj_par: bit-identical, for the bench-size checks).
+        Returns the step-major states after 0, snap_every, 2*snap_every, ...
+        steps, shape (num_steps // snap_every + 1, m)."""
+        if threads is None:
+            n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 1
+            omp = os.environ.get("OMP_NUM_THREADS", "")
+            threads = max(1, min(n, int(omp))) if omp.isdigit() else n
+        out = np.empty((num_steps // snap_every + 1, self.m))
+        lib().orc_march_traj_par(*self._c(), _p(np.ascontiguousarray(w0, dtype=np.float64)),
+                                 int(num_steps), int(snap_every), _p(out), int(threads))
+        return out
+
     def fom(self, w0, num_steps, solver="march", max_its=100, cutoff=1e-12):
         """Step-major trajectory (num_steps+1, m) + Newton counts/rels."""
         snaps = np.empty((num_steps + 1, self.m))

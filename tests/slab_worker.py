@@ -2,7 +2,7 @@
 its slab of an NX x NY grid (default N x N), T steps from w0 = 1, on device 0,
 rendezvous over gloo; writes its slab snapshot matrix.
 
-    slab_worker.py N T OUTDIR [run|sweep]
+    slab_worker.py N T OUTDIR [run|sweep|residual|failstate]
     env: SLAB_NY (rows, default N), SLAB_W (pipe tile width, 0 = plan),
          SLAB_TILES (tiles target per rank), SLAB_SNAP_EVERY (default 1),
          SLAB_DT (default 0.05); writes slab{rank}.npy, .w (tile width) and
@@ -38,6 +38,24 @@ def main():
     ctx.set_problem(gx, gy, dt, (5.19, 0.026), allow_nonsquare=(ny != N))
     w0 = slab_state(np.ones(2 * N * ny), N, ny, rank, world)
     dist.barrier()
+    mode = sys.argv[4] if len(sys.argv) > 4 else "run"
+    if mode == "failstate":
+        # BURG_TEST_FAIL_DEVICE_HALO=1: the first launch fails as a stalled
+        # device halo ring would; the context must then refuse to launch
+        from finitedifference_amd._lib import BurgersError
+        codes = []
+        for _ in range(2):
+            try:
+                ctx.run(w0, T)
+                codes.append(0)
+            except BurgersError as e:
+                codes.append(e.code)
+        with open(os.path.join(out, f"slab{rank}.codes"), "w") as f:
+            f.write(" ".join(map(str, codes)))
+        dist.barrier()
+        ctx.close()
+        dist.destroy_process_group()
+        return
     if sweep:
         snaps, st = ctx.sweep(SWEEP_MUS, T, w0=w0, snap_every=every)
         assert st["engine"] == 2
@@ -47,6 +65,22 @@ def main():
         snaps, st, _, _ = ctx.run(w0, T, snap_every=every)
         assert st["engine"] == 2
         np.save(os.path.join(out, f"slab{rank}.npy"), snaps)
+        if mode == "residual":
+            # the slab residual of the last step with the halo rows sent by
+            # the rank below (burg_slab_residual + send/recv over gloo)
+            from finitedifference_amd.dist import (exchange_halo_rows, slab_residual_norms,
+                                                   top_row)
+            rows = ctx.ny
+            wT, wP = snaps[:, -1].copy(), snaps[:, -2].copy()
+            got = exchange_halo_rows(np.concatenate((top_row(wT, N, rows), top_row(wP, N, rows))),
+                                     N, rank, world, dist)
+            halo = (None, None) if got is None else (got[:2 * N], got[2 * N:])
+            r, ss = ctx.slab_residual(wT, wP, *halo)
+            np.save(os.path.join(out, f"slab{rank}_res.npy"), r)
+            g1, s1 = slab_residual_norms(ctx, wT, wP, dist)
+            g0, s0 = slab_residual_norms(ctx, wP, wP, dist)
+            with open(os.path.join(out, f"slab{rank}.norms"), "w") as f:
+                f.write(" ".join(repr(x) for x in (ss, g1, s1, g0, s0)))
     with open(os.path.join(out, f"slab{rank}.w"), "w") as f:
         f.write(str(st["stream_w"]))
     with open(os.path.join(out, f"slab{rank}.halo"), "w") as f:

@@ -1077,7 +1077,9 @@ def test_plot_snaps_slices(gpu):
 def test_snapshot_cache_snap_every_and_short_files(gpu, tmp_path):
     """load_or_compute_snaps: a thinned (snap_every > 1) run is cached under a
     name of its own, never under the reference's per-step name; a cached file
-    with too few columns is recomputed, not returned short."""
+    with too few columns is returned short, as the reference does
+    (C/hypernet2D.py:3138, np.load(fn)[:, :num_steps+1]), and recomputed only
+    with recompute_short=True."""
     from finitedifference_amd import hypernet2D as H
     N, T = 32, 12
     gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
@@ -1091,8 +1093,12 @@ def test_snapshot_cache_snap_every_and_short_files(gpu, tmp_path):
     full = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d)
     assert full.shape[1] == T + 1 and np.array_equal(full[:, ::4], thin)
     np.save(os.path.join(d, "mu1_5.19+mu2_0.026.npy"), full[:, :5])  # a short cache
-    again = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d)
+    short = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d)
+    assert np.array_equal(short, full[:, :5])
+    again = H.load_or_compute_snaps((5.19, 0.026), gx, gy, w0, 0.05, T, snap_folder=d,
+                                    recompute_short=True)
     assert np.array_equal(again, full)
+    assert np.load(os.path.join(d, "mu1_5.19+mu2_0.026.npy")).shape[1] == T + 1
 
 
 def test_direct_npy_writer(gpu, tmp_path, monkeypatch):

@@ -257,3 +257,20 @@ def test_oracle_under_sanitizers():
                        text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "sanitize_check ok" in r.stdout
+
+
+@pytest.mark.parametrize("nx,ny,T,every,threads", [(37, 23, 5, 1, 3), (200, 130, 7, 2, 8),
+                                                   (64, 64, 4, 4, 5), (130, 1, 3, 1, 4)])
+def test_row_pipelined_march_is_the_serial_march(orc, nx, ny, T, every, threads):
+    """orc_march_traj_par (rows pipelined over OpenMP threads; the checker of
+    the bench-size GPU trajectories in tests/test_gpu_regime.py) equals
+    orc_march_step's trajectory bit for bit, including tiny/subnormal states
+    (the IEEE slow path's inputs)."""
+    P = orc.Problem(nx, ny, Ly=100.0 * ny / nx, allow_nonsquare=nx != ny)
+    w0 = np.ones(P.m)
+    w0[nx * ny:][::7] = 5e-320
+    ref, _, _ = P.fom(w0, T)
+    out = P.march_traj(w0, T, every, threads=threads)
+    assert out.shape == (T // every + 1, P.m)
+    for j in range(out.shape[0]):
+        assert np.array_equal(out[j], ref[j * every]), j
