@@ -1131,6 +1131,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         } else {
             run_block(Interior(), sb);
         }
+        // a steady block advances the ring pointer without wrapping (it may
+        // end exactly at the ring's end: the next store goes to entry 0)
+        if (steady && pw == Lu) pw = 0u;
     }
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, spins);
