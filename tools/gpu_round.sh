@@ -7,7 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${TAG:-round}
 mkdir -p $O
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
 tail -3 $O/pytest_gpu.log
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
 cat $O/smoke.log
@@ -16,7 +16,7 @@ cat $O/bench.json
 # the N > 1 bench path (slab contexts, halo self-test, max-over-ranks timing)
 # rehearsed with 2 ranks sharing the box's GPU (gloo; W = 128 so both slabs'
 # workgroups are resident together)
-timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rehearse-one-gpu --nx 2048 --rows-per-gpu 1024 --stream-w 128 --steps 5 --warmup 1 > $O/bench_rehearse_n2.json 2> $O/bench_rehearse.err || { tail -20 $O/bench_rehearse.err; exit 1; }
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --rehearse-one-gpu --nx 8192 --rows-per-gpu 256 --stream-w 128 --steps 5 --warmup 1 > $O/bench_rehearse_n2.json 2> $O/bench_rehearse.err || { tail -20 $O/bench_rehearse.err; exit 1; }
 cat $O/bench_rehearse_n2.json
 # the same with every device-ring launch failing (test hook): the bench must
 # fall back to the host rings on all ranks and still print its line
