@@ -83,6 +83,13 @@ struct StreamStats {
 // Bytes per edge granule slot: one 128-B L2 line each, so that reading one
 // granule never caches a neighbour granule before its producer wrote it.
 constexpr int kGranuleStride = 128;
+// pipe engine mailboxes: granules packed 16 B apart (a poll of 16 consecutive
+// diagonals fetches 2 lines instead of 16; -DBURG_PIPE_G=128 for the round-2
+// layout, one granule per line)
+#ifndef BURG_PIPE_G
+#define BURG_PIPE_G 16
+#endif
+constexpr int kPipeGranuleStride = BURG_PIPE_G;
 
 struct StreamPlan {
     int W, nti, ntj, ntiles, R;

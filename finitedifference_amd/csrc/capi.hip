@@ -404,7 +404,7 @@ int stream_setup(burg_ctx *c)
             c->sp = pp;
             c->nwj = wj;
             c->eng_eff = BURG_ENGINE_PIPE;
-            c->box16 = (size_t)pp.ntiles * kPipeR * (kWave + pp.W) * (kGranuleStride / sizeof(d2));
+            c->box16 = (size_t)pp.ntiles * kPipeR * (kWave + pp.W) * (kPipeGranuleStride / sizeof(d2));
             if (c->box16 * sizeof(d2) >= (1ull << 31))
                 return fail(BURG_ESHAPE, "edge mailboxes exceed 2 GiB");
             if (int e = dalloc(&c->d_boxes, c->box16)) return e;
@@ -512,9 +512,9 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.colc = c->d_colc;
     a.ring = c->d_ring;
     a.wbox = c->d_boxes;
-    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * kPipeR * kWave * (kGranuleStride / sizeof(d2));
-    a.wbox_bytes = (size_t)c->sp.ntiles * kPipeR * kWave * kGranuleStride;
-    a.sbox_bytes = (size_t)c->sp.ntiles * kPipeR * c->sp.W * kGranuleStride;
+    a.sbox = c->d_boxes + (size_t)c->sp.ntiles * kPipeR * kWave * (kPipeGranuleStride / sizeof(d2));
+    a.wbox_bytes = (size_t)c->sp.ntiles * kPipeR * kWave * kPipeGranuleStride;
+    a.sbox_bytes = (size_t)c->sp.ntiles * kPipeR * c->sp.W * kPipeGranuleStride;
     a.halo_in = c->halo_in_dev;
     a.halo_out = c->halo_out_dev;
     a.halo_bytes = c->halo_bytes;

@@ -90,7 +90,7 @@ constexpr unsigned kLdsEmptyHi = 0x7FF6DEADu;  // LDS slot empty
 constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, stores dropped
 constexpr int kR = kPipeR;
 constexpr int kRL = kPipeRL;
-constexpr unsigned G = kGranuleStride;
+constexpr unsigned G = kPipeGranuleStride;
 template <int W>
 constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
 constexpr int kNI = 64;   // south inbox ring (diagonals), power of two

@@ -35,11 +35,83 @@ __device__ __forceinline__ double ror1(double x)
     return __hiloint2double(hi, lo);
 }
 
+// MarchCell::chain<true> for two independent cells, statement by statement
+// interleaved (same op order per cell: bit-identical results)
+__device__ __forceinline__ void chain2_fast(const MarchCell::Pre &pa, const MarchCell::Pre &pb,
+                                            const MarchCell::Row &rw, const double *e0, const double *e1,
+                                            const double *n0, const double *n1, double *oe0, double *oe1,
+                                            double *on0, double *on1, double *o0, double *o1, bool &ok)
+{
+    const MarchCell::Pre *p[2] = {&pa, &pb};
+    double cu[2], cv[2], q[2], y[2], g[2], h[2], r[2], d[2], s[2], rc[2], e[2], t0[2], t1[2], m0[2],
+        m1[2], nu[2], nv[2], hxu[2];
+    unsigned bad = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) cu[k] = (p[k]->bu + e0[k]) + n0[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) cv[k] = (p[k]->bv + n1[k]) + e1[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) q[k] = 0.25 + fma(p[k]->hx, cu[k], rw.hy * cv[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const unsigned hu = (unsigned)__double2hiint(cu[k]), hv = (unsigned)__double2hiint(cv[k]);
+        const unsigned hq = (unsigned)__double2hiint(q[k]);
+        const unsigned eu = ((hu - (123u << 20)) >> 20) & 0x7FFu;
+        const unsigned ev = ((hv - (123u << 20)) >> 20) & 0x7FFu;
+        const unsigned eq = (hq - (123u << 20)) >> 20;
+        bad |= max(max(eu, ev), eq);
+    }
+    ok = bad < 1800u;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) y[k] = __builtin_amdgcn_rsq(q[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) { g[k] = q[k] * y[k]; h[k] = y[k] * 0.5; }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) r[k] = fma(-h[k], g[k], 0.5);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) { g[k] = fma(g[k], r[k], g[k]); h[k] = fma(h[k], r[k], h[k]); }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) d[k] = fma(-g[k], g[k], q[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) g[k] = fma(d[k], h[k], g[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) d[k] = fma(-g[k], g[k], q[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) s[k] = 0.5 + fma(d[k], h[k], g[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rc[k] = __builtin_amdgcn_rcp(s[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) e[k] = fma(-s[k], rc[k], 1.0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rc[k] = fma(rc[k], e[k], rc[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) e[k] = fma(-s[k], rc[k], 1.0);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) rc[k] = fma(rc[k], e[k], rc[k]);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) { t0[k] = cu[k] * rc[k]; t1[k] = cv[k] * rc[k]; }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) { m0[k] = fma(-s[k], t0[k], cu[k]); m1[k] = fma(-s[k], t1[k], cv[k]); }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) { nu[k] = fma(m0[k], rc[k], t0[k]); nv[k] = fma(m1[k], rc[k], t1[k]); }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) hxu[k] = p[k]->hx * nu[k];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        oe0[k] = fma(hxu[k], nu[k], p[k]->xfp);
+        oe1[k] = fma(hxu[k], nv[k], p[k]->xhp);
+        on0[k] = fma(rw.hy * nu[k], nv[k], p[k]->yhp);
+        on1[k] = fma(rw.hy * nv[k], nv[k], p[k]->ygp);
+        o0[k] = nu[k];
+        o1[k] = nv[k];
+    }
+}
+
 struct Cell {
     double e0, e1, no0, no1;
 };
 
-template <int SETS>
+template <int SETS, bool IL>
 __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *ring, long long *cyc,
                                                     long long *ieee)
 {
@@ -77,10 +149,16 @@ __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *
             n0[k] = shr1_or(ror1(cs[k - 1].no0), cs[k].no0);
             n1[k] = shr1_or(ror1(cs[k - 1].no1), cs[k].no1);
         }
+        if constexpr (SETS == 2 && IL) {
+            const double e0[2] = {cs[0].e0, cs[1].e0}, e1[2] = {cs[0].e1, cs[1].e1};
+            chain2_fast(p[0], p[1], rw, e0, e1, n0, n1, oe0, oe1, on0, on1, o0, o1, ok[0]);
+            ok[1] = ok[0];
+        } else {
 #pragma unroll
-        for (int k = 0; k < SETS; ++k)
-            MarchCell::chain<true>(p[k], rw, cs[k].e0, cs[k].e1, n0[k], n1[k], oe0[k], oe1[k], on0[k],
-                                   on1[k], o0[k], o1[k], ok[k]);
+            for (int k = 0; k < SETS; ++k)
+                MarchCell::chain<true>(p[k], rw, cs[k].e0, cs[k].e1, n0[k], n1[k], oe0[k], oe1[k], on0[k],
+                                       on1[k], o0[k], o1[k], ok[k]);
+        }
         bool allok = true;
 #pragma unroll
         for (int k = 0; k < SETS; ++k) allok = allok && ok[k];
@@ -107,7 +185,7 @@ __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *
     }
 }
 
-template <int SETS>
+template <int SETS, bool IL = false>
 void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long *d_ieee)
 {
     std::vector<long long> cyc(blocks * 4), ie(blocks * 4);
@@ -116,7 +194,7 @@ void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long 
     (void)hipEventCreate(&b);
     for (int rep = 0; rep < 3; ++rep) {
         (void)hipEventRecord(a);
-        hipLaunchKernelGGL(chain_kernel<SETS>, dim3(blocks), dim3(256), 0, 0, d_in, d_ring, d_cyc, d_ieee);
+        hipLaunchKernelGGL((chain_kernel<SETS, IL>), dim3(blocks), dim3(256), 0, 0, d_in, d_ring, d_cyc, d_ieee);
         (void)hipEventRecord(b);
         (void)hipEventSynchronize(b);
     }
@@ -128,9 +206,9 @@ void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long 
     for (long long c : cyc) avg += (double)c;
     avg /= cyc.size();
     // s_memtime ticks at 100 MHz on gfx950? report ns per diagonal from events too
-    printf("sets=%d blocks=%d: %.1f memtime ticks per diagonal per wave, %.1f ns per diagonal "
+    printf("sets=%d%s blocks=%d: %.1f memtime ticks per diagonal per wave, %.1f ns per diagonal "
            "(events), cells per ns chip-wide %.2f, ieee=%lld\n",
-           SETS, blocks, avg / kD, ms * 1e6 / kD, (double)blocks * 4 * 64 * SETS * kD / (ms * 1e6),
+           SETS, IL ? " interleaved" : "", blocks, avg / kD, ms * 1e6 / kD, (double)blocks * 4 * 64 * SETS * kD / (ms * 1e6),
            ie[0]);
 }
 
@@ -149,6 +227,7 @@ int main()
     for (int blocks : {1, 256}) {
         run<1>(blocks, d_in, d_ring, d_cyc, d_ieee);
         run<2>(blocks, d_in, d_ring, d_cyc, d_ieee);
+        run<2, true>(blocks, d_in, d_ring, d_cyc, d_ieee);
     }
     return 0;
 }
