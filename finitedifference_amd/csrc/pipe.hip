@@ -277,7 +277,9 @@ struct PipeLds {
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
     // wide: previous states by diagonal, filled by LDS-DMA -- first in the
     // image: the DMA's LDS address comes from M0[15:0] (the 64 KB below 2^16)
-    v4u win[4][WIDE ? win_of<W>() : 1][WIDE ? kWave : 1];
+    // (narrow tiles: unused by the window; its 8 entries hold the zero south
+    // inflow of a boundary strip, read by block offsets -- see zeros)
+    v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : 8];
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
@@ -289,8 +291,7 @@ struct PipeLds {
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
-    v4u zeros[WIDE ? 8 : W == 8 ? 1 : BURG_NARROW_U];  // south inflow of a boundary strip,
-                                                       // read by block offsets
+    v4u zeros[WIDE ? 8 : 1];  // wide: south inflow of a boundary strip, read by block offsets
     // write target of lanes with nothing to hand off (W = 8 runs no steady
     // blocks: its image must fit three times in a CU)
     v4u dump[W == 8 ? 1 : kWave];
@@ -388,7 +389,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         sm.filled[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
-    if (threadIdx.x < (WIDE ? 8 : W == 8 ? 1 : BURG_NARROW_U)) sm.zeros[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
+    static_assert(WIDE || BURG_NARROW_U <= 8, "narrow blocks read at most 8 zero inflows");
+    if (threadIdx.x < 8) (WIDE ? &sm.zeros[0] : &sm.win[0][0][0])[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
     if constexpr (SWEEP) {
@@ -762,7 +764,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if constexpr (WIDE) b.wb = &sm.win[k][sb % KWIN][lane];
         else b.wb = (LDS v4u *)&my_st[(sb & (W - 1)) * kWave + lane];
         b.cb = &sm.cc[k][(sb - lane) & (W - 1)];
-        b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : &sm.zeros[0];
+        b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : WIDE ? &sm.zeros[0] : &sm.win[0][0][0];
         b.c0 = (sb - lane) & (W - 1);
         return b;
     };

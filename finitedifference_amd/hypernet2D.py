@@ -94,10 +94,12 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     par_passes); solver="newton" runs the reference algorithm
     (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
     Both return the reference's snapshot matrix.  verbose=1 (default) prints
-    what the reference prints: the header line, then per step
+    what the reference prints, unchanged: the header line, then per step
     " ... Working on timestep i" (C/hypernet2D.py:122) and, for the newton
     solver, Newton's "k: rel" line (:1844) -- after the run, since the whole
-    time loop is one launch; verbose=0 prints nothing.  out: an existing
+    time loop is one launch.  The march solver runs no Newton iteration, so
+    it prints no Newton line (it does not emulate one); verbose=0 prints
+    nothing.  out: an existing
     (2n, num_steps//snap_every + 1) C-contiguous float64 array (e.g. a .npy
     memmap) the snapshots are written into and returned.
     """
