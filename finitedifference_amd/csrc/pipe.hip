@@ -99,7 +99,7 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #define BURG_KLA 16
 #endif
 #ifndef BURG_NARROW_U
-#define BURG_NARROW_U 4
+#define BURG_NARROW_U 8
 #endif
 constexpr int kLA = BURG_KLA;  // poll window (diagonals ahead of a compute wave's progress)
 // Wide tiles run one workgroup per CU with a 16-diagonal window and blocks of

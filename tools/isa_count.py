@@ -109,7 +109,7 @@ def main():
     res = {"source": "tools/isa_count.py (hipcc -O3 --offload-arch=gfx950 -save-temps of pipe.hip)",
            "issue_model": "4 cycles per instruction + 12 per fp64 transcendental (one wave per SIMD)"}
     for W, sweep in ((256, False), (16, True), (16, False)):
-        U = 8 if W > 16 else 4  # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U)
+        U = 8  # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U, 8 since round 3)
         rr = [r[i:i + U] for r in runs(kernel_body(asm, W, sweep)) for i in range(0, len(r), U)]
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
