@@ -553,7 +553,7 @@ def main():
         if st["engine"] == 2:
             clk, csrc = read_clock(args.pmc_file, key)
             iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + nx + rows,
-                                 args.isa_file, st["stream_w"], U=8 if st["stream_w"] > 16 else 4,
+                                 args.isa_file, st["stream_w"], U=8,
                                  clock_ghz=clk, clock_src=csrc)
             if iss:
                 out["issue_roofline"] = iss
@@ -639,7 +639,7 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
     kname = f"pipe_kernel<{st['stream_w']}, true>"
     clk, csrc = read_clock(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
     iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 2 * nx, isa_file,
-                         st["stream_w"], U=8 if st["stream_w"] > 16 else 4, clock_ghz=clk,
+                         st["stream_w"], U=8, clock_ghz=clk,
                          clock_src=csrc) if isa_file else None
     return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
             "issue_roofline": iss,

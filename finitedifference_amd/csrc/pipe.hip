@@ -98,6 +98,10 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #ifndef BURG_KLA
 #define BURG_KLA 16
 #endif
+// cache policy of the wide tiles' ring stores (16: sc1, write-through)
+#ifndef BURG_RING_AUX
+#define BURG_RING_AUX 16
+#endif
 #ifndef BURG_NARROW_U
 #define BURG_NARROW_U 8
 #endif
@@ -279,14 +283,15 @@ struct PipeLds {
     // image: the DMA's LDS address comes from M0[15:0] (the 64 KB below 2^16)
     // (narrow tiles: unused by the window; its 8 entries hold the zero south
     // inflow of a boundary strip, read by block offsets -- see zeros)
-    v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : 8];
+    v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : BURG_NARROW_U];
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
-    v4u cc[4][W + (W == 8 ? 0 : 8)];  // per wave: {hx, src} of the tile's columns, + the
-                                      // first 8 again, so a steady block's lane reads
-                                      // base + u unwrapped (W = 8: no steady blocks)
+    // per wave: {hx, src} of the tile's columns, + the first kPad again, so a
+    // steady block's lane reads base + u unwrapped (W = 8: no steady blocks)
+    static constexpr int kPad = W == 8 ? 0 : (WIDE ? 8 : BURG_NARROW_U);
+    v4u cc[4][W + kPad];
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
@@ -294,7 +299,10 @@ struct PipeLds {
     v4u zeros[WIDE ? 8 : 1];  // wide: south inflow of a boundary strip, read by block offsets
     // write target of lanes with nothing to hand off (W = 8 runs no steady
     // blocks: its image must fit three times in a CU)
-    v4u dump[W == 8 ? 1 : kWave];
+    // (narrow 16-diagonal sweep blocks: 16 slots shared by 4 lanes each, the
+    // room their longer column padding needs)
+    static constexpr int kDump = W == 8 ? 1 : (!WIDE && SWEEP && BURG_NARROW_U > 8) ? 16 : kWave;
+    v4u dump[kDump];
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
     int prog[4];            // per compute wave: first diagonal of its current block
@@ -325,7 +333,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
     static_assert(!(WIDE && SWEEP), "parameter sweeps run on narrow tiles");
     constexpr int LW = ilog2<W>();
-    constexpr int U = WIDE ? uw_of<W>() : BURG_NARROW_U;  // diagonals per block (progress published per block)
+    // diagonals per block (progress published per block); narrow: at most W, so
+    // a lane meets column 0 at most once per block
+    constexpr int U = WIDE ? uw_of<W>() : (BURG_NARROW_U < W ? BURG_NARROW_U : W);
     constexpr int KWIN = win_of<W>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -389,8 +399,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         sm.filled[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
-    static_assert(WIDE || BURG_NARROW_U <= 8, "narrow blocks read at most 8 zero inflows");
-    if (threadIdx.x < 8) (WIDE ? &sm.zeros[0] : &sm.win[0][0][0])[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
+    if (threadIdx.x < (WIDE ? 8 : BURG_NARROW_U))
+        (WIDE ? &sm.zeros[0] : &sm.win[0][0][0])[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;
     if constexpr (SWEEP) {
@@ -408,7 +418,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
-        for (int c = lane; c < W + (W == 8 ? 0 : 8); c += kWave) {
+        for (int c = lane; c < W + PipeLds<W, SWEEP>::kPad; c += kWave) {
             const d2 v = a.colc[(size_t)(tj0 + wave) * W + (c & (W - 1))];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
@@ -905,11 +915,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // diagonals later, so it is stored write-through to L2 (sc1): the
         // store's vmcnt then completes at L2, which the done[] protocol needs
         if constexpr (STEADY) {
-            if constexpr (WIDE) st_dev_so(ring, lane16, pw * 1024u, out);
+            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(out, ring, lane16, pw * 1024u, BURG_RING_AUX);
             else st_plain_so(ring, lane16, pw * 1024u, out);
             ++pw;  // (no wrap inside a steady block)
         } else {
-            if constexpr (WIDE) st_dev(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(out, ring, valid ? pw * 1024u + lane16 : kOOB, 0, BURG_RING_AUX);
             else st_plain(ring, valid ? pw * 1024u + lane16 : kOOB, out);
             pw = pw + 1 == Lu ? 0u : pw + 1;
         }
@@ -918,9 +928,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
         if constexpr (SE) {
-            lds_st(atE ? se_eaddr : &sm.dump[lane], eo);
+            lds_st(atE ? se_eaddr : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
         } else if constexpr (WIDE) {
-            if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane], eo);
+            if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
         } else {
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
         }
@@ -956,7 +966,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // consumed inbound slots back to empty (steady-edge blocks: once per
         // block, run_block)
         if constexpr (WIDE || STEADY) {
-            if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane], lempty);
+            if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], lempty);
             // (the south slots are freed once per block, run_block)
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
@@ -1014,7 +1024,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 se_in = has_west & (se_uw < U);
                 const bool oute = se_ue < U;
                 se_gw = lds_ld(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.zero);
-                se_eaddr = (east_lds & oute) ? &sm.ewe[k][qe & (kRL - 1)][lane] : &sm.dump[lane];
+                se_eaddr = (east_lds & oute) ? &sm.ewe[k][qe & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
                 se_eoff = (east_glob & oute) ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             }
             const Bases b = bases_of(sb);
@@ -1029,13 +1039,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             }
             // SteadyEdge: the west granule consumed in this block back to empty
             if (decltype(tag)::value == 3 && has_west)
-                lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane], lempty);
+                lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], lempty);
         }
         if constexpr (WIDE || decltype(tag)::value == 3) {
             // the block's south inbox slots back to empty, one write: lane i
             // frees diagonal sb + i's slot
             if (has_south)
-                lds_st(((lane < U) & (sb + lane < KW)) ? &sm.ins[k][(sb + lane) & (kNI - 1)] : &sm.dump[lane],
+                lds_st(((lane < U) & (sb + lane < KW)) ? &sm.ins[k][(sb + lane) & (kNI - 1)] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)],
                        lempty);
         }
     };

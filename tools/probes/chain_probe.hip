@@ -111,7 +111,7 @@ struct Cell {
     double e0, e1, no0, no1;
 };
 
-template <int SETS, bool IL>
+template <int SETS, bool IL, int ST = 1>
 __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *ring, long long *cyc,
                                                     long long *ieee)
 {
@@ -174,8 +174,12 @@ __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *
             cs[k] = Cell{(s & (kW - 1)) == kW - 1 ? 0.0 : oe0[k], (s & (kW - 1)) == kW - 1 ? 0.0 : oe1[k],
                          on0[k], on1[k]};
             st[wave][k][s & (kW - 1)][lane] = make_double2(o0[k], o1[k]);
-            __builtin_nontemporal_store(o0[k], &my[((size_t)k * kD + s) * 64 + lane].x);
-            __builtin_nontemporal_store(o1[k], &my[((size_t)k * kD + s) * 64 + lane].y);
+            if constexpr (ST == 1) {
+                __builtin_nontemporal_store(o0[k], &my[((size_t)k * kD + s) * 64 + lane].x);
+                __builtin_nontemporal_store(o1[k], &my[((size_t)k * kD + s) * 64 + lane].y);
+            } else if constexpr (ST == 2) {  // plain (cached) stores
+                my[((size_t)k * kD + s) * 64 + lane] = make_double2(o0[k], o1[k]);
+            }
         }
     }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
@@ -185,7 +189,7 @@ __global__ __launch_bounds__(256) void chain_kernel(const double *cin, double2 *
     }
 }
 
-template <int SETS, bool IL = false>
+template <int SETS, bool IL = false, int ST = 1>
 void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long *d_ieee)
 {
     std::vector<long long> cyc(blocks * 4), ie(blocks * 4);
@@ -194,7 +198,7 @@ void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long 
     (void)hipEventCreate(&b);
     for (int rep = 0; rep < 3; ++rep) {
         (void)hipEventRecord(a);
-        hipLaunchKernelGGL((chain_kernel<SETS, IL>), dim3(blocks), dim3(256), 0, 0, d_in, d_ring, d_cyc, d_ieee);
+        hipLaunchKernelGGL((chain_kernel<SETS, IL, ST>), dim3(blocks), dim3(256), 0, 0, d_in, d_ring, d_cyc, d_ieee);
         (void)hipEventRecord(b);
         (void)hipEventSynchronize(b);
     }
@@ -206,9 +210,9 @@ void run(int blocks, double *d_in, double2 *d_ring, long long *d_cyc, long long 
     for (long long c : cyc) avg += (double)c;
     avg /= cyc.size();
     // s_memtime ticks at 100 MHz on gfx950? report ns per diagonal from events too
-    printf("sets=%d%s blocks=%d: %.1f memtime ticks per diagonal per wave, %.1f ns per diagonal "
+    printf("sets=%d%s store=%d blocks=%d: %.1f memtime ticks per diagonal per wave, %.1f ns per diagonal "
            "(events), cells per ns chip-wide %.2f, ieee=%lld\n",
-           SETS, IL ? " interleaved" : "", blocks, avg / kD, ms * 1e6 / kD, (double)blocks * 4 * 64 * SETS * kD / (ms * 1e6),
+           SETS, IL ? " interleaved" : "", ST, blocks, avg / kD, ms * 1e6 / kD, (double)blocks * 4 * 64 * SETS * kD / (ms * 1e6),
            ie[0]);
 }
 
@@ -228,6 +232,8 @@ int main()
         run<1>(blocks, d_in, d_ring, d_cyc, d_ieee);
         run<2>(blocks, d_in, d_ring, d_cyc, d_ieee);
         run<2, true>(blocks, d_in, d_ring, d_cyc, d_ieee);
+        run<1, false, 0>(blocks, d_in, d_ring, d_cyc, d_ieee);
+        run<1, false, 2>(blocks, d_in, d_ring, d_cyc, d_ieee);
     }
     return 0;
 }
