@@ -115,7 +115,10 @@ struct StreamArgs {
 // Same tiles and ring as the streaming engine; a workgroup holds 4 adjacent
 // tiles of one strip (4 compute waves) plus one comm wave.  Global mailboxes
 // use two sentinel colours so that a slot's emptiness is tied to a step.
-constexpr int kPipeR = 8;   // global mailbox slots (steps) per edge, power of two
+#ifndef BURG_PIPE_R
+#define BURG_PIPE_R 8
+#endif
+constexpr int kPipeR = BURG_PIPE_R;  // global mailbox slots (steps) per edge, power of two
 constexpr int kPipeRL = 4;  // LDS ring slots (steps) per intra-workgroup edge
 constexpr int kPipeSweepMax = 9;   // trajectories per sweep launch (LDS-resident tables)
 

@@ -217,7 +217,7 @@ __device__ __forceinline__ void st_sys(__amdgpu_buffer_rsrc_t rs, unsigned off, 
 }
 // the same stores with a scalar offset part (soffset): a per-lane offset that
 // stays constant over a block, a per-diagonal one in an SGPR
-__device__ __forceinline__ void st_dev_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
+[[maybe_unused]] __device__ __forceinline__ void st_dev_so(__amdgpu_buffer_rsrc_t rs, unsigned voff, unsigned soff, v4u v)
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 16);
 }
@@ -730,6 +730,19 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // branch), and the inlet term added at column 0 (0 off the inlet tile)
     unsigned nv1 = kOOB, nv2 = kOOB;
     double lb_se = 0.0;
+    // a column's {hx, src}; sweeps take src from their per-trajectory tables,
+    // so they load hx alone (a dead src half would be a register the compiler
+    // reuses while the load is in flight: an LDS wait per diagonal)
+    auto cc_ld = [&](const LDS v4u *p) -> v4u {
+        if constexpr (SWEEP) {
+            typedef unsigned v2u __attribute__((ext_vector_type(2)));
+            const v2u x = *(const LDS v2u *)p;
+            return v4u{x.x, x.y, 0u, 0u};
+        } else {
+            return *p;
+        }
+    };
+
     auto fetch = [&](auto edge_tag, int s) -> In {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
@@ -752,7 +765,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.src = 0.0;
             in.xs = lds_ld(&sm.win[k][s % KWIN][lane]);
         }
-        in.cs = sm.cc[k][c];
+        in.cs = cc_ld(&sm.cc[k][c]);
         if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
         else in.gw = v4u{0u, 0u, 0u, 0u};
         in.gs = lds_ld((has_south & (STEADY || s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
@@ -789,7 +802,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.src = src_cur[c];
         }
         in.xs = lds_ld(b.wb + u * kWave);
-        in.cs = b.cb[u];
+        in.cs = cc_ld(b.cb + u);
         in.gw = v4u{0u, 0u, 0u, 0u};
         in.gs = lds_ld(b.ib + u);
         return in;
