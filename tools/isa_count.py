@@ -61,7 +61,9 @@ def runs(lines):
     """Unrolled fast-path blocks: maximal runs of consecutive segments between
     v_rsq_f64 of the cell chain that are not IEEE re-runs (v_div_scale /
     v_div_fixup of the compiler's division).  The last segment of a run also
-    holds the loop tail and the next block's head (readiness check, loads)."""
+    holds the loop tail and the next block's head (readiness check, loads);
+    the readiness-wait loop (nested loop depth >= 2) is not counted (round 3:
+    round 2's counts included it)."""
     rs = [k for k, l in enumerate(lines) if "v_rsq_f64" in l]
     out, cur = [], []
     for a, b in zip(rs, rs[1:] + [len(lines)]):
@@ -71,8 +73,18 @@ def runs(lines):
                 out.append(cur)
             cur = []
             continue
-        cur.append([l.strip().split()[0] for l in seg
-                    if l.strip() and not l.strip().startswith((".", ";"))])
+        # skip the readiness-wait loop (basic blocks nested at loop depth >= 2:
+        # code that runs only while a block waits, not per diagonal)
+        ins, inner = [], False
+        for l in seg:
+            t = l.strip()
+            if t.startswith(".LBB"):
+                m = re.search(r"Depth=(\d+)", t)
+                inner = bool(m) and int(m.group(1)) >= 2
+                continue
+            if t and not t.startswith((".", ";")) and not inner:
+                ins.append(t.split()[0])
+        cur.append(ins)
     if cur:
         out.append(cur)
     return [r for r in out if len(r) >= 4]
