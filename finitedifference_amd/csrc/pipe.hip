@@ -890,8 +890,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         }
         const MarchCell::Row rw{ay, hy, lbu};
         // ---- the cell's chain
-        if (at0) {
+        // (steady blocks: a select, not an exec-masked move -- the compiler
+        // guards the masked form with a branch, taken on most diagonals)
+        if constexpr (STEADY) {
             const d2 gv = as_d2(SE ? se_gw : in.gw);
+            e0 = at0 ? gv.x : e0;
+            e1 = at0 ? gv.y : e1;
+        } else if (at0) {
+            const d2 gv = as_d2(in.gw);
             e0 = gv.x;
             e1 = gv.y;
         }
@@ -951,12 +957,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // are dropped): exactly 3 per edge and 2 per interior diagonal, which
         // the vmcnt of done[] counts
         if constexpr (SE) {
-            // (wide: every diagonal issues the same number of stores, for done[])
-            if (WIDE || east_glob) st_dev(wbox, atE ? se_eoff : kOOB, eo);
+            // (wide: every diagonal issues the same number of stores, for done[];
+            // narrow: unconditional too -- se_eoff is out of range unless this is
+            // the workgroup's east wave -- a dropped store costs less than the
+            // two taken branches around a conditional one)
+            st_dev(wbox, atE ? se_eoff : kOOB, eo);
         }
         else if (EDGE && (WIDE || east_glob))
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
-        if (WIDE || has_north) {
+        // (narrow steady blocks store unconditionally: nv1 / nv2 are out of
+        // range on every lane but a north-writing top lane)
+        if (WIDE || STEADY || has_north) {
             // one store flavour for both targets: sc0 sc1 (system scope) reaches
             // the host / peer halo ring and is write-through like sc1 for the
             // device mailboxes (consumers poll with sc1 / sc0 sc1 loads)

@@ -25,7 +25,7 @@ SRC = os.path.join(ROOT, "finitedifference_amd", "csrc", "pipe.hip")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-ffp-contract=off",
          "-Wno-bitwise-instead-of-logical",
          "-mllvm", "-amdgpu-sched-strategy=max-ilp"]  # as the Makefile builds pipe.hip
-FLAGS_NARROW = FLAGS[:-2]
+FLAGS_NARROW = FLAGS  # (round 3: both pipe units use max-ilp, Makefile)
 SRC_NARROW = os.path.join(ROOT, "finitedifference_amd", "csrc", "pipe_narrow.hip")
 
 
@@ -109,8 +109,8 @@ def main():
     ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "pipe_isa.json"))
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
-        # wide kernels: pipe.hip with max-ilp; narrow: pipe_narrow.hip with the
-        # default scheduler (as the Makefile builds them)
+        # pipe.hip (wide kernels) and pipe_narrow.hip (narrow), both with
+        # max-ilp, as the Makefile builds them
         subprocess.run(["/opt/rocm/bin/hipcc", *FLAGS, "-c", SRC, "-o", os.path.join(d, "p.o"),
                         "-save-temps"], cwd=d, check=True, capture_output=True)
         asm = open(os.path.join(d, "pipe-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
