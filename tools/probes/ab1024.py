@@ -19,12 +19,16 @@ ctx.set_problem(g, g, 0.05, (5.19, 0.026))
 ctx.upload(np.ones(ctx.m))
 mus = get_snapshot_params()[:9]
 ctx.sweep(mus, 500, keep_snaps=False)
-sw = [ctx.sweep(mus, 500, keep_snaps=False)[1]["loop_ms"] for _ in range(reps)]
+sws = [ctx.sweep(mus, 500, keep_snaps=False)[1] for _ in range(reps)]
+sw = [x["loop_ms"] for x in sws]
 c1 = float(np.sum(ctx.download()))
 ctx.trajectory(500)
-tr = [ctx.trajectory(500)["loop_ms"] for _ in range(reps)]
+trs = [ctx.trajectory(500) for _ in range(reps)]
+tr = [x["loop_ms"] for x in trs]
 c2 = float(np.sum(ctx.download()))
 tag = os.environ.get("BURG_LIB", "default").split("/")[-1]
 print(f"{tag}: 1024^2 sweep {min(sw):.2f} ms ({nx*nx*4500/min(sw)/1e6:.1f} Gcell/s) | single traj "
-      f"{min(tr):.3f} ms ({nx*nx*500/min(tr)/1e6:.1f} Gcell/s) | checksums {c1:.17g} {c2:.17g}",
+      f"{min(tr):.3f} ms ({nx*nx*500/min(tr)/1e6:.1f} Gcell/s) | checksums {c1:.17g} {c2:.17g} | ieee "
+      f"{sws[-1]['ieee_diagonals']} {trs[-1]['ieee_diagonals']} blocked {sws[-1]['slow_diagonals']} "
+      f"{trs[-1]['slow_diagonals']}",
       flush=True)
