@@ -1277,6 +1277,14 @@ int burg_set_problem(burg_ctx *c, const double *inv_dx, const double *inv_dy,
     if (!c) return fail(BURG_EINVAL, "null context");
     if (!inv_dx || !inv_dy || !src || !lbc) return fail(BURG_EINVAL, "null coefficient array");
     if (!(dt > 0.0) || !std::isfinite(dt)) return fail(BURG_EINVAL, "dt must be > 0");
+    // the march cell's fast window (cell_math.h) relies on h_x = dt/4 / dx and
+    // h_y = dt/4 / dy in (0, 2^100): q then stays finite and >= 0.25
+    for (int i = 0; i < c->nx; ++i)
+        if (!(0.25 * dt * inv_dx[i] > 0.0 && 0.25 * dt * inv_dx[i] < 0x1p100))
+            return fail(BURG_EINVAL, "dt/dx out of range (0, 2^102) at column %d", i);
+    for (int i = 0; i < c->ny_total; ++i)
+        if (!(0.25 * dt * inv_dy[i] > 0.0 && 0.25 * dt * inv_dy[i] < 0x1p100))
+            return fail(BURG_EINVAL, "dt/dy out of range (0, 2^102) at row %d", i);
     HIPCHK(hipSetDevice(c->device));
     if (!c->d_inv_dx) {
         if (int e = dalloc(&c->d_inv_dx, (size_t)c->nx)) return e;

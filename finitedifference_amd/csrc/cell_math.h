@@ -129,24 +129,21 @@ struct MarchCell {
         const double q = 0.25 + mm;
         double s, nu, nv;
         if constexpr (FAST) {
-            // Cu, Cv of magnitude in [2^-900, 2^900): div2_normal's exact range;
-            // q in [2^-900, 2^900) and positive: sqrt_normal's (q = 0.25 + mm is
-            // either <= 0 or >= 2^-55 by Sterbenz, so this is q > 0 short of
-            // overflow).  Zeros, -0 (it would come out +0), denormals, Inf and
-            // NaN fail and go to the IEEE path, which reports a NaN.  Tested on
-            // the exponent fields of the high words: subtracting 123 << 20 and
-            // extracting bits 20..30 gives e - 123 for a biased exponent
-            // e >= 123 and >= 1925 below (the borrow), whatever the sign, so
-            // |x| passes iff that field is < 1800 (e in [123, 1922]); q keeps
-            // its sign bit, which puts a negative q out of its window.  Integer
-            // VALU and two compares instead of seven fp64 compares and their
-            // mask arithmetic.
-            const unsigned hu = (unsigned)__double2hiint(cu), hv = (unsigned)__double2hiint(cv);
-            const unsigned hq = (unsigned)__double2hiint(q);
-            const unsigned eu = ((hu - (123u << 20)) >> 20) & 0x7FFu;
-            const unsigned ev = ((hv - (123u << 20)) >> 20) & 0x7FFu;
-            const unsigned eq = (hq - (123u << 20)) >> 20;  // sign bit kept: negative q >= 2048
-            range_ok = max(max(eu, ev), eq) < 1800u;        // one v_max3 and one compare
+            // The fast window: Cu, Cv POSITIVE with magnitude in [2^-900,
+            // 2^900), div2_normal's exact range.  Then q = 0.25 + h_x Cu + h_y Cv
+            // is >= 0.25 (h_x, h_y > 0) and finite (h_x, h_y < 2^100, checked by
+            // burg_set_problem), inside sqrt_normal's exact range, and s =
+            // 0.5 + sqrt(q) >= 1: no test of q is needed.  Tested on the high
+            // words: less 123 << 20, a positive operand's word is below
+            // 1800 << 20 iff its biased exponent is in [123, 1922] (a smaller
+            // one borrows past the top, a negative one has the top bit set).
+            // Zeros, negatives, denormals, Inf and NaN take the IEEE path
+            // (which reports a NaN): the reference regime's velocities are
+            // positive, and a negative Cu / Cv is still computed exactly.  Two
+            // subtracts, a max and a compare.
+            const unsigned xu = (unsigned)__double2hiint(cu) - (123u << 20);
+            const unsigned xv = (unsigned)__double2hiint(cv) - (123u << 20);
+            range_ok = max(xu, xv) < (1800u << 20);
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {
