@@ -851,6 +851,37 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         return why;
     };
 
+    // The same test, fused for the common case: every kind's per-lane
+    // condition folded into one predicate, read without branches (an LDS load
+    // of a kind the wave has no edge for reads a harmless slot) and decided
+    // by ONE ballot -- block_missing's per-kind branches and ballots (each an
+    // i1 -> VGPR -> compare -> SCC round trip in the compiler's hands) cost
+    // tens of instructions per block.  block_missing then only runs when a
+    // block has to wait (it names the missing kinds).
+    auto block_ready = [&](int sb) -> bool {
+        const int t0 = sb - lane;
+        const int c0 = t0 & (W - 1);
+        const int uw = (W - c0) & (W - 1);
+        const int tw = t0 + uw;
+        const v4u g = lds_ld(&src_w[(tw >> LW) & (kRL - 1)][lane]);
+        const bool miss_w = has_west & (uw < U) & ((unsigned)tw < (unsigned)KW) & rowok & !l_is_data(g);
+        const int d = sb + lane;
+        const unsigned hs = lds_ld32((const LDS char *)&sm.ins[k][d & (kNI - 1)] + 4);
+        const bool miss_s = has_south & (lane < U) & (d < KW) & (hs == kLdsEmptyHi);
+        const int ue = (W - 1 - c0) & (W - 1);
+        const int te = t0 + ue;
+        const bool oe = (ue < U) & ((unsigned)te < (unsigned)KW) & rowok;
+        const unsigned he = lds_ld32((const LDS char *)&sm.ewe[east_lds ? k : 0][(te >> LW) & (kRL - 1)][lane] + 4);
+        const int pe = lds_ldi(&sm.pe_row[lane]);
+        const bool miss_e = oe & ((east_lds & (he != kLdsEmptyHi)) | (east_glob & ((te >> LW) >= pe)));
+        const int pn = lds_ldi(&sm.perm[k]);
+        const int th = min(sb - top + U - 1, KW - 1);
+        const bool miss_n = has_north & (th >= 0) & (th >= pn);
+        bool miss = miss_w | miss_s | miss_e | miss_n;
+        if constexpr (WIDE) miss = miss | (lds_ldi(&sm.filled[k]) < sb + U);
+        return __builtin_amdgcn_ballot_w64(miss) == 0;
+    };
+
     // one diagonal, diagonal u of its block (no waits: the block was checked)
     auto diagonal = [&](auto edge_tag, const int s, const int u, In &in) {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
@@ -1099,22 +1130,25 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (lane == 0) lds_sti(&sm.done[k], sb - U);
         }
         if (lane == 0) lds_sti(&sm.prog[k], sb);
-        unsigned why = block_missing(sb);
-        if (__builtin_expect(why != 0, 0)) {
-            const long long t0 = now_rt();
-            const unsigned long long c0 = __builtin_amdgcn_s_memtime();
-            ++slow_n;
-            wait_why[0] += (why & 12u) != 0;  // east (LDS ring or global grant)
-            wait_why[1] += (why & 16u) != 0;  // north grant
-            wait_why[2] += (why & 1u) != 0;   // west inflow
-            wait_why[3] += (why & 2u) != 0;   // south inflow
-            wait_why[4] += (why & 32u) != 0;  // previous states (loader window)
+        if (__builtin_expect(!block_ready(sb), 0)) {
+            // (block_missing runs inside the wait loop, out of the hot path)
+            long long t0 = 0;
+            unsigned long long c0 = 0;
+            bool waited = false;
             for (;;) {
-                ++spins;
-                __builtin_amdgcn_s_sleep(1);
-                why = block_missing(sb);
+                const unsigned why = block_missing(sb);
                 if (!why) break;
-                if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
+                if (!waited) {
+                    waited = true;
+                    t0 = now_rt();
+                    c0 = __builtin_amdgcn_s_memtime();
+                    ++slow_n;
+                    wait_why[0] += (why & 12u) != 0;  // east (LDS ring or global grant)
+                    wait_why[1] += (why & 16u) != 0;  // north grant
+                    wait_why[2] += (why & 1u) != 0;   // west inflow
+                    wait_why[3] += (why & 2u) != 0;   // south inflow
+                    wait_why[4] += (why & 32u) != 0;  // previous states (loader window)
+                } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                     if (lane == 0 && !lds_ldi(&sm.perm[5])) {
                         lds_sti(&sm.perm[5], 1);
                         if (atomicOr(a.err, 1u) == 0) {
@@ -1126,8 +1160,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     aborted = true;
                     break;
                 }
+                ++spins;
+                __builtin_amdgcn_s_sleep(1);
             }
-            wait_ticks += __builtin_amdgcn_s_memtime() - c0;
+            if (waited) wait_ticks += __builtin_amdgcn_s_memtime() - c0;
             if (aborted) break;
         }
         const int sm_ = sb & (W - 1);

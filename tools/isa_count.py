@@ -1,16 +1,22 @@
 """Instruction counts of the pipe kernel's diagonal, from its gfx950 ISA.
 
-Compiles finitedifference_amd/csrc/pipe.hip with -save-temps, takes the
-unrolled fast-path blocks of pipe_kernel<W, SWEEP> (runs of the code between
-consecutive v_rsq_f64 of the cell chain, block overhead included) and counts
-instructions by kind, averaged per diagonal.
+Compiles finitedifference_amd/csrc/pipe.hip and pipe_narrow.hip with
+-save-temps (as the Makefile builds them), splits each pipe_kernel<W, SWEEP>
+into basic blocks and, for every fast block of U diagonals (U consecutive
+v_rsq_f64 of the cell chain outside the IEEE re-run and the readiness-wait
+loop), counts the instructions of one loop iteration through it: the
+cheapest path over hot blocks from the compute loop's header to the block's
+first diagonal, diagonal to diagonal, and back (round 3; until then the code
+between consecutive v_rsq_f64 in layout order, which also counted cold code
+the compiler placed there).  The cheapest path may skip guarded blocks a wave
+does run, so the counts are lower bounds.  Averaged per diagonal by kind.
 Writes profiles/<round>/pipe_isa.json, which bench.py turns into the
 `issue` roofline: one wave alone issues at most one instruction per 4 cycles
 (fp64 FMA measured at 4.3, v_rsq_f64 / v_rcp_f64 at ~16: tools/probes/
 issue_probe.hip), so 4 cycles x instructions (+12 per transcendental) is the
 per-diagonal floor of a compute wave.
 
-    python tools/isa_count.py [--out profiles/r02/pipe_isa.json]
+    python tools/isa_count.py [--out profiles/r03/pipe_isa.json]
 """
 import argparse
 import collections
@@ -90,6 +96,132 @@ def runs(lines):
     return [r for r in out if len(r) >= 4]
 
 
+def parse_blocks(lines):
+    """Basic blocks of a kernel body: label -> block, in layout order.  Each
+    block: its instructions (opcode strings), loop depth, whether it is cold
+    (the IEEE re-run, the readiness-wait loop, abort paths), successors."""
+    blocks, cur = [], None
+
+    def start(label, depth):
+        b = {"label": label, "ins": [], "depth": depth, "succ": []}
+        blocks.append(b)
+        return b
+
+    for ln in lines:
+        t = ln.strip()
+        is_lbl = t.startswith(".LBB") and t.split()[0].endswith(":")
+        if is_lbl or t.startswith("; %bb."):
+            m = re.search(r"Depth=(\d+)", t)
+            label = t.split()[0].rstrip(":") if is_lbl else None
+            cur = start(label, int(m.group(1)) if m else 0)
+            if re.search(r"Loop Header: Depth=1\b", t):
+                cur["header"] = True
+            continue
+        if not t or t.startswith((".", ";")):
+            if cur is not None and re.search(r"Loop Header: Depth=1\b", t):
+                cur["header"] = True  # (the header comment on its own line)
+            continue
+        if cur is None or (cur["ins"] and cur["ins"][-1].startswith(("s_branch", "s_cbranch"))):
+            cur = start(None, cur["depth"] if cur else 0)
+        cur["ins"].append(t.split()[0] if not t.startswith(("s_branch", "s_cbranch")) else t)
+    idx = {b["label"]: i for i, b in enumerate(blocks) if b["label"]}
+    for i, b in enumerate(blocks):
+        last = b["ins"][-1] if b["ins"] else ""
+        nxt = [i + 1] if i + 1 < len(blocks) else []
+        if last.startswith("s_branch"):
+            b["succ"] = [idx[last.split()[1]]]
+        elif last.startswith("s_cbranch"):
+            b["succ"] = [idx[last.split()[1]]] + nxt
+        elif last.startswith(("s_endpgm", "s_setpc")):
+            b["succ"] = []
+        else:
+            b["succ"] = nxt
+        b["ins"] = [x.split()[0] for x in b["ins"]]
+        b["cold"] = b["depth"] >= 2 or any(
+            o.startswith(("v_div_scale", "v_div_fixup"))
+            for o in b["ins"])
+    return blocks
+
+
+def hot_cycle(blocks, U):
+    """Per fast run of U diagonals (U consecutive v_rsq_f64 outside the cold
+    blocks): the instructions one loop iteration through that run executes --
+    the cheapest path over hot blocks from the compute loop's header to the
+    run's first diagonal, from diagonal to diagonal, and back to the header
+    (routing never passes the header in between).  Returns per-diagonal
+    opcode lists (the header-to-first-rsq and last-rsq-to-header code in the
+    last diagonal's list, as runs() does)."""
+    import heapq
+    rsq = [(i, j) for i, b in enumerate(blocks) if not b["cold"]
+           for j, o in enumerate(b["ins"]) if o.startswith("v_rsq_f64")]
+    # the compute loop's header: of the depth-1 loop headers, the one the
+    # most runs close a cycle through (the comm and loader loops close none)
+    best = []
+    for H in [i for i, b in enumerate(blocks) if b.get("header")]:
+        r = _cycles(blocks, U, rsq, H)
+        if len(r) > len(best):
+            best = r
+    return best
+
+
+def _cycles(blocks, U, rsq, H):
+    import heapq
+
+    def path(a, z):
+        # the CHEAPEST a -> z path over hot blocks (z's instructions included,
+        # a's not; never through the header in between): a lower bound of
+        # what a wave executes -- guarded blocks a wave does run (an
+        # exec-masked store, a check of an edge it has) may be skipped, so the
+        # issue roofline built on this count is conservative
+        dist, prev, pq = {a: 0}, {}, [(0, a)]
+        while pq:
+            d, u = heapq.heappop(pq)
+            if u == z and u in prev:
+                break
+            if d > dist.get(u, 1 << 60):
+                continue
+            for v in blocks[u]["succ"]:
+                if blocks[v]["cold"] or (v == H and z != H):
+                    continue
+                nd = d + len(blocks[v]["ins"]) + 1
+                if nd < dist.get(v, 1 << 60) or (v == z and v == a and v not in prev):
+                    dist[v], prev[v] = nd, u
+                    heapq.heappush(pq, (nd, v))
+        if z not in prev:
+            return None
+        out, v = [z], prev[z]
+        while v != a:
+            out.append(v)
+            v = prev[v]
+        return out[::-1]
+
+    # group the hot rsq's into runs of U (in layout order)
+    res = []
+    for g in range(0, len(rsq) - U + 1, U):
+        run = rsq[g:g + U]
+        seq = [H] + (path(H, run[0][0]) or [])
+        ok = len(seq) > 1 or run[0][0] == H
+        for (b0, _), (b1, _) in zip(run, run[1:]):
+            p = path(b0, b1) if b1 != b0 else []
+            if p is None:
+                ok = False
+                break
+            seq += p
+        back = path(run[-1][0], H)
+        if not ok or back is None:
+            continue
+        seq += back[:-1]  # (the header is seq[0])
+        ops = [o for bi in seq for o in blocks[bi]["ins"]]
+        # rotate to start at the run's first rsq, split at each rsq
+        pos = [k for k, o in enumerate(ops) if o.startswith("v_rsq_f64")]
+        if len(pos) != U:
+            continue
+        ops = ops[pos[0]:] + ops[:pos[0]]
+        pos = [p - pos[0] for p in pos] + [len(ops)]
+        res.append([ops[pos[i]:pos[i + 1]] for i in range(U)])
+    return res
+
+
 def summarise(run):
     """Per-block totals of one unrolled run (U diagonals)."""
     c = collections.Counter()
@@ -106,7 +238,7 @@ def summarise(run):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "pipe_isa.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03", "pipe_isa.json"))
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         # pipe.hip (wide kernels) and pipe_narrow.hip (narrow), both with
@@ -122,7 +254,7 @@ def main():
            "issue_model": "4 cycles per instruction + 12 per fp64 transcendental (one wave per SIMD)"}
     for W, sweep in ((256, False), (16, True), (16, False)):
         U = 8  # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U, 8 since round 3)
-        rr = [r[i:i + U] for r in runs(kernel_body(asm, W, sweep)) for i in range(0, len(r), U)]
+        rr = hot_cycle(parse_blocks(kernel_body(asm, W, sweep)), U)
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
         names = {1: ["block"], 2: ["steady_edge_block", "edge_block"] if W <= 16 else
