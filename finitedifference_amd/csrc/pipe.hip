@@ -93,7 +93,6 @@ constexpr int kRL = kPipeRL;
 constexpr unsigned G = kPipeGranuleStride;
 template <int W>
 constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
-constexpr int kNI = 64;   // south inbox ring (diagonals), power of two
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
 #ifndef BURG_KLA
 #define BURG_KLA 16
@@ -273,6 +272,16 @@ constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
 template <int W>
 constexpr bool is_wide() { return W > 16; }
 
+// south inbox ring (diagonals): a power of two above the comm wave's poll
+// window plus a block; 32 for the narrow sweep kernel, whose LDS image is full
+// (the room pads its per-trajectory source rows, read by block offsets)
+template <int W, bool SWEEP>
+constexpr int ni_of() { return (!is_wide<W>() && SWEEP) ? 32 : 64; }
+// sweep source rows: W columns + the first kSrcPad again (steady blocks read
+// base + u unwrapped, as the column table)
+template <int W, bool SWEEP>
+constexpr int src_pad_of() { return (!is_wide<W>() && SWEEP) ? BURG_NARROW_U : 0; }
+
 // LDS image of one workgroup (SWEEP: a parameter sweep, burg_sweep -- the
 // initial state and every trajectory's source / inlet terms stay on chip)
 template <int W, bool SWEEP>
@@ -286,7 +295,7 @@ struct PipeLds {
     v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : BURG_NARROW_U];
     v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
     v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
-    double srcb[kSW][4][SWEEP ? W : 1];            // sweep: src of trajectory j, by column
+    double srcb[kSW][4][SWEEP ? W + src_pad_of<W, SWEEP>() : 1];  // sweep: src of trajectory j, by column
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
     // per wave: {hx, src} of the tile's columns, + the first kPad again, so a
     // steady block's lane reads base + u unwrapped (W = 8: no steady blocks)
@@ -294,14 +303,17 @@ struct PipeLds {
     v4u cc[4][W + kPad];
     v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
-    v4u ins[4][kNI];        // south inflow of each wave, by diagonal (comm wave deposits)
+    v4u ins[4][ni_of<W, SWEEP>()];  // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
     v4u zeros[WIDE ? 8 : 1];  // wide: south inflow of a boundary strip, read by block offsets
     // write target of lanes with nothing to hand off (W = 8 runs no steady
     // blocks: its image must fit three times in a CU)
     // (narrow 16-diagonal sweep blocks: 16 slots shared by 4 lanes each, the
     // room their longer column padding needs)
-    static constexpr int kDump = W == 8 ? 1 : (!WIDE && SWEEP && BURG_NARROW_U > 8) ? 16 : kWave;
+    // (narrow sweeps: 32 slots, two lanes each -- lanes 32 apart, in
+    // different passes of a b128 write -- the room their padded source rows
+    // need)
+    static constexpr int kDump = W == 8 ? 1 : (!WIDE && SWEEP) ? (BURG_NARROW_U > 8 ? 16 : 32) : kWave;
     v4u dump[kDump];
     int perm[8];            // [0..3] north grants per wave (diagonal), [4] east grant of wave 3
                             // (step), [5] abort
@@ -337,6 +349,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // a lane meets column 0 at most once per block
     constexpr int U = WIDE ? uw_of<W>() : (BURG_NARROW_U < W ? BURG_NARROW_U : W);
     constexpr int KWIN = win_of<W>();
+    constexpr int kNI = ni_of<W, SWEEP>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -405,9 +418,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const int nsw = SWEEP ? a.K / a.T : 1;
     if constexpr (SWEEP) {
         const size_t ncolp = (size_t)ntj * W;
-        for (int i = threadIdx.x; i < nsw * 4 * W; i += kThreads) {
-            const int j = i / (4 * W), kc = i - j * 4 * W;
-            const int kk = kc / W, c = kc - kk * W;
+        constexpr int WS = W + src_pad_of<W, SWEEP>();
+        for (int i = threadIdx.x; i < nsw * 4 * WS; i += kThreads) {
+            const int j = i / (4 * WS), kc = i - j * 4 * WS;
+            const int kk = kc / WS, c = (kc - kk * WS) & (W - 1);
             (&sm.srcb[0][0][0])[i] = tj0 + kk < ntj ? a.colc_b[j * ncolp + (size_t)(tj0 + kk) * W + c].y
                                                     : 0.0;
         }
@@ -778,6 +792,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // into the LDS instructions' immediate fields.
     struct Bases {
         LDS v4u *wb, *cb, *ib;
+        lds_f64 *sr;  // sweep: the lane's source row at its first column of the block
         int c0;  // the lane's column at the block's first diagonal
     };
     auto bases_of = [&](int sb) -> Bases {
@@ -789,18 +804,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         b.cb = &sm.cc[k][(sb - lane) & (W - 1)];
         b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : WIDE ? &sm.zeros[0] : &sm.win[0][0][0];
         b.c0 = (sb - lane) & (W - 1);
+        b.sr = src_cur + b.c0;  // (padded row: + u does not wrap)
         return b;
     };
     auto fetch_b = [&](const Bases &b, int u) -> In {
         In in;
         in.nt = false;
         in.src = 0.0;
-        if constexpr (SWEEP) {
-            // the trajectory's source by column: the lane's column wraps to 0
-            // at diagonal se_uw of the block (the table is not padded)
-            const int c = ((b.c0 + u) & (W - 1));
-            in.src = src_cur[c];
-        }
+        if constexpr (SWEEP) in.src = b.sr[u];  // (no trajectory switch in the block)
         in.xs = lds_ld(b.wb + u * kWave);
         in.cs = cc_ld(b.cb + u);
         in.gw = v4u{0u, 0u, 0u, 0u};
@@ -1106,6 +1117,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     };
 
     const int total = KW + kWave - 1;
+    LDS int *const sink_i = (LDS int *)&sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
     // Land the prologue's global loads (row coefficients) here: a first use
     // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
     // in flight -- into every diagonal.
@@ -1127,9 +1139,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 #ifdef BURG_PIPE_PROF
             pf_vm += __builtin_amdgcn_s_memtime() - pfa;
 #endif
-            if (lane == 0) lds_sti(&sm.done[k], sb - U);
+            lds_sti(lane == 0 ? &sm.done[k] : sink_i, sb - U);
         }
-        if (lane == 0) lds_sti(&sm.prog[k], sb);
+        // (every lane stores -- lane 0 the progress, the others into their
+        // dump slot -- instead of an exec-masked branch around one store)
+        lds_sti(lane == 0 ? &sm.prog[k] : sink_i, sb);
         if (__builtin_expect(!block_ready(sb), 0)) {
             // (block_missing runs inside the wait loop, out of the hot path)
             long long t0 = 0;
@@ -1176,10 +1190,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // narrow tiles (U <= W: a lane meets column 0 at most once per block)
         // run steady-edge blocks too; sweeps only where no lane is in the
         // first step of its next trajectory (that step reads the initial state)
-        bool steady = nrow == kWave && sb >= kWave && sb + U <= KW && pw + U <= Lu &&
-                      ((!WIDE && north_dev) || ct0 + U <= min(W, ncol_real));
+        // (bitwise, not short-circuit: scalar ops and one branch, not a chain)
+        bool steady = (nrow == kWave) & (sb >= kWave) & (sb + U <= KW) & (pw + U <= Lu) &
+                      ((!WIDE & north_dev) | (ct0 + U <= min(W, ncol_real)));
         if constexpr (SWEEP)
-            steady = steady && !any_lane(((sb + U - 1 - lane) >> LW) >= qn);
+            steady = steady & !any_lane(((sb + U - 1 - lane) >> LW) >= qn);
         if (steady)
         {
             noffs = nb + (unsigned)((a.qbase + (tt0 >> LW)) & (kR - 1)) * nstep + (unsigned)ct0 * ncol;
