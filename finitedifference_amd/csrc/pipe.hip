@@ -730,6 +730,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // block-constant diagonals (uw, ue) and steps -- its west granule is read
     // once, its hand-off addresses are fixed, the inputs come by block base
     typedef std::integral_constant<int, 3> SteadyEdge;
+    typedef std::integral_constant<int, 4> SteadyEdgeG;  // (the east wave's build)
     int se_uw = U, se_ue = U;  // SteadyEdge: the lane's column-0 / column-(W-1) diagonal in the block
     v4u se_gw = v4u{0u, 0u, 0u, 0u};
     LDS v4u *se_eaddr = nullptr;
@@ -896,7 +897,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // one diagonal, diagonal u of its block (no waits: the block was checked)
     auto diagonal = [&](auto edge_tag, const int s, const int u, In &in) {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
-        constexpr bool SE = decltype(edge_tag)::value == 3;
+        constexpr bool SE = decltype(edge_tag)::value >= 3;
+        // (narrow steady-edge blocks come in two builds: 4 for the
+        // workgroup's east wave, whose east outflow goes to the global
+        // mailbox, 3 for the others, whose outflow goes to the LDS ring --
+        // each issues only its own; wide tiles run 3 only, with both)
+        constexpr bool SE_G = decltype(edge_tag)::value == 4;
         constexpr bool STEADY = decltype(edge_tag)::value >= 2;
         const int t = s - lane;
         const int c = t & (W - 1);
@@ -989,7 +995,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
         if constexpr (SE) {
-            lds_st(atE ? se_eaddr : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
+            if constexpr (!SE_G) lds_st(atE ? se_eaddr : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
         } else if constexpr (WIDE) {
             if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
         } else {
@@ -1003,7 +1009,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // narrow: unconditional too -- se_eoff is out of range unless this is
             // the workgroup's east wave -- a dropped store costs less than the
             // two taken branches around a conditional one)
-            st_dev(wbox, atE ? se_eoff : kOOB, eo);
+            if (WIDE || SE_G) st_dev(wbox, atE ? se_eoff : kOOB, eo);
         }
         else if (EDGE && (WIDE || east_glob))
             st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
@@ -1059,14 +1065,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // diagonal: a lane's trajectory switch (in diagonal s) decides which
     // state and source table diagonal s + 1 reads.
     auto run_block = [&](auto tag, const int sb) {
-        if constexpr (SWEEP && decltype(tag)::value != 3) {
+        if constexpr (SWEEP && decltype(tag)::value < 3) {
             In a0 = fetch(tag, sb);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 diagonal(tag, sb + u, u, a0);
                 if (u + 1 < U) a0 = fetch(tag, sb + u + 1);
             }
-        } else if constexpr ((!WIDE && decltype(tag)::value != 3) || decltype(tag)::value == 0) {
+        } else if constexpr ((!WIDE && decltype(tag)::value < 3) || decltype(tag)::value == 0) {
             In a0 = fetch(tag, sb), a1 = fetch(tag, sb + 1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -1079,7 +1085,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         } else {
             int se_qw = 0;
             bool se_in = false;
-            if constexpr (decltype(tag)::value == 3) {
+            if constexpr (decltype(tag)::value >= 3) {
                 if constexpr (!WIDE) lb_se = col0_tile ? lb : 0.0;  // (no switch inside)
                 // the lane's column-0 and column-(W-1) cells in this block
                 const int c0 = (sb - lane) & (W - 1);
@@ -1104,10 +1110,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 if (u + 2 < U) a1 = nx;
             }
             // SteadyEdge: the west granule consumed in this block back to empty
-            if (decltype(tag)::value == 3 && has_west)
+            if (decltype(tag)::value >= 3 && has_west)
                 lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], lempty);
         }
-        if constexpr (WIDE || decltype(tag)::value == 3) {
+        if constexpr (WIDE || decltype(tag)::value >= 3) {
             // the block's south inbox slots back to empty, one write: lane i
             // frees diagonal sb + i's slot
             if (has_south)
@@ -1211,8 +1217,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if (!WIDE || W <= kWave || sm_ < kWave || sm_ == W - U) {
             // (narrow-or-equal tiles, W <= 64: one block's lanes span several
             // steps, so the steady offsets do not hold -- plain edge blocks)
-            if ((W == 16 || W > kWave) && steady) run_block(SteadyEdge(), sb);
-            else run_block(Edge(), sb);
+            if ((W == 16 || W > kWave) && steady) {
+                // (narrow tiles only: the wide kernel measured 0.6 % slower
+                // with the two builds, profiles/r03/ab/steady_edge_east.txt)
+                if (!WIDE && east_glob) run_block(SteadyEdgeG(), sb);
+                else run_block(SteadyEdge(), sb);
+            } else {
+                run_block(Edge(), sb);
+            }
         } else if (steady) {
             run_block(Steady(), sb);
         } else {

@@ -257,10 +257,16 @@ def main():
         rr = hot_cycle(parse_blocks(kernel_body(asm, W, sweep)), U)
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
+        # (steady-edge blocks are built twice since round 3: for the
+        # workgroup's east wave -- "_east", outflow to the global mailbox --
+        # and for the others; the two differ by a store and a select)
         names = {1: ["block"], 2: ["steady_edge_block", "edge_block"] if W <= 16 else
                  ["interior_block", "edge_block"],
-                 3: ["steady_block", "interior_block", "edge_block"],
-                 4: ["steady_block", "interior_block", "steady_edge_block", "edge_block"]}[len(rr)]
+                 3: ["steady_edge_block", "steady_edge_block_east", "edge_block"] if W <= 16 else
+                 ["steady_block", "interior_block", "edge_block"],
+                 4: ["steady_block", "interior_block", "steady_edge_block", "edge_block"],
+                 5: ["steady_block", "interior_block", "steady_edge_block", "steady_edge_block_east",
+                     "edge_block"]}[len(rr)]
         res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}>"] = {
             "per_diagonal_averages": {nm: summarise(r) for nm, r in zip(names, rr)}}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
