@@ -233,6 +233,12 @@ def end_to_end(nx=1024, T=500):
                     "matrix (burg_run_npy)"}
 
 
+def block_of(W):
+    """Diagonals per readiness block of the pipe kernel (pipe.hip uw_of):
+    16 for wide tiles of 128 and 256 columns, 8 otherwise (round 3)."""
+    return 16 if W in (128, 256) else 8
+
+
 def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=None, clock_src=None):
     """Issue bound of the march kernel's compute waves: instructions per
     diagonal from the kernel's ISA (tools/isa_count.py -> profiles/r02/
@@ -553,7 +559,7 @@ def main():
         if st["engine"] == 2:
             clk, csrc = read_clock(args.pmc_file, key)
             iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + nx + rows,
-                                 args.isa_file, st["stream_w"], U=8,
+                                 args.isa_file, st["stream_w"], U=block_of(st["stream_w"]),
                                  clock_ghz=clk, clock_src=csrc)
             if iss:
                 out["issue_roofline"] = iss
@@ -639,7 +645,7 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
     kname = f"pipe_kernel<{st['stream_w']}, true>"
     clk, csrc = read_clock(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
     iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 2 * nx, isa_file,
-                         st["stream_w"], U=8, clock_ghz=clk,
+                         st["stream_w"], U=block_of(st["stream_w"]), clock_ghz=clk,
                          clock_src=csrc) if isa_file else None
     return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
             "issue_roofline": iss,

@@ -89,7 +89,6 @@ constexpr unsigned kSentLo = 0xBEEF5A5Au;
 constexpr unsigned kLdsEmptyHi = 0x7FF6DEADu;  // LDS slot empty
 constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, stores dropped
 constexpr int kR = kPipeR;
-constexpr int kRL = kPipeRL;
 constexpr unsigned G = kPipeGranuleStride;
 template <int W>
 constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
@@ -104,7 +103,10 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #ifndef BURG_NARROW_U
 #define BURG_NARROW_U 8
 #endif
-constexpr int kLA = BURG_KLA;  // poll window (diagonals ahead of a compute wave's progress)
+// the comm wave's poll window (diagonals ahead of a compute wave's progress):
+// at least two blocks, so the next block's inflows arrive during this one
+template <int W>
+constexpr int la_of();
 // Wide tiles run one workgroup per CU with a 16-diagonal window and blocks of
 // 8.  Built with -DBURG_TWO_PER_CU=1, W = 64 and 128 run two workgroups per CU
 // instead (two compute waves per SIMD: one wave's scalar, LDS and memory
@@ -116,12 +118,35 @@ constexpr int kLA = BURG_KLA;  // poll window (diagonals ahead of a compute wave
 #ifndef BURG_TWO_PER_CU
 #define BURG_TWO_PER_CU 0
 #endif
+// the wide tiles' window of previous states, diagonals per compute wave: a
+// multiple of the block -- the loader fills up to KWIN - U diagonals ahead of
+// the block being computed (W = 1024: 16, its column table takes the room; 24
+// for W <= 512 measured no faster than 16)
+#ifndef BURG_KWIN
+#define BURG_KWIN 16
+#endif
 template <int W>
 constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
+// Blocks of 16 diagonals for W = 128, 256 (round 3; window 32 diagonals, LDS
+// rings of 2 steps between the workgroup's waves -- the room for it; the LDS
+// DMA reaches past 64 KB, tools/probes/dma_high_probe.hip): the block head is
+// paid once per 16 diagonals -- 4096^2 53.0 -> 49.0 ms per trajectory
+// (profiles/r03/ab/wide_u16.txt).  W = 512, 1024 keep blocks of 8 (their
+// column tables leave no room for a 32-diagonal window).
+#ifndef BURG_WIDE_U16
+#define BURG_WIDE_U16 1
+#endif
 template <int W>
-constexpr int win_of() { return two_per_cu<W>() ? 12 : 16; }  // window (diagonals)
+constexpr bool u16_of() { return BURG_WIDE_U16 && !two_per_cu<W>() && (W == 128 || W == 256); }
 template <int W>
-constexpr int uw_of() { return two_per_cu<W>() ? 4 : 8; }  // block (diagonals)
+constexpr int win_of() { return two_per_cu<W>() ? 12 : u16_of<W>() ? 32 : W >= 1024 ? 16 : BURG_KWIN; }  // window (diagonals)
+template <int W>
+constexpr int uw_of() { return two_per_cu<W>() ? 4 : u16_of<W>() ? 16 : 8; }  // block (diagonals)
+template <int W>
+constexpr int la_of() { return u16_of<W>() ? 32 : BURG_KLA; }
+// LDS ring slots (steps) of the intra-workgroup west -> east edges
+template <int W>
+constexpr int rl_of() { return u16_of<W>() ? 2 : kPipeRL; }
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt at their maximum (no wait): gfx9
 // encoding vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.  A
@@ -299,13 +324,13 @@ struct PipeLds {
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
     // per wave: {hx, src} of the tile's columns, + the first kPad again, so a
     // steady block's lane reads base + u unwrapped (W = 8: no steady blocks)
-    static constexpr int kPad = W == 8 ? 0 : (WIDE ? 8 : BURG_NARROW_U);
+    static constexpr int kPad = W == 8 ? 0 : (WIDE ? uw_of<W>() : BURG_NARROW_U);
     v4u cc[4][W + kPad];
-    v4u ewe[3][kRL][kWave]; // wave k -> k+1 east outflow, by step slot and row
-    v4u inw[kRL][kWave];    // west inflow of wave 0 (comm wave deposits)
+    v4u ewe[3][rl_of<W>()][kWave]; // wave k -> k+1 east outflow, by step slot and row
+    v4u inw[rl_of<W>()][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][ni_of<W, SWEEP>()];  // south inflow of each wave, by diagonal (comm wave deposits)
     v4u zero;               // inflow at the domain boundary
-    v4u zeros[WIDE ? 8 : 1];  // wide: south inflow of a boundary strip, read by block offsets
+    v4u zeros[WIDE ? uw_of<W>() : 1];  // wide: south inflow of a boundary strip, read by block offsets
     // write target of lanes with nothing to hand off (W = 8 runs no steady
     // blocks: its image must fit three times in a CU)
     // (narrow 16-diagonal sweep blocks: 16 slots shared by 4 lanes each, the
@@ -333,8 +358,7 @@ template <int W, bool SWEEP>
 __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 {
     constexpr int kThreads = threads_of<W>();
-    static_assert(!is_wide<W>() || sizeof(PipeLds<W, SWEEP>::win) <= 65536,
-                  "LDS-DMA window must sit below 64 KB");
+    static_assert(win_of<W>() % uw_of<W>() == 0, "the window holds whole blocks");
     static_assert(sizeof(PipeLds<W, SWEEP>) <= 160 * 1024, "LDS image exceeds the CU's 160 KiB");
     constexpr bool WIDE = is_wide<W>();
     // three narrow W=8 workgroups per CU: room for 8 slab processes sharing one
@@ -350,6 +374,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     constexpr int U = WIDE ? uw_of<W>() : (BURG_NARROW_U < W ? BURG_NARROW_U : W);
     constexpr int KWIN = win_of<W>();
     constexpr int kNI = ni_of<W, SWEEP>();
+    constexpr int kRL = rl_of<W>();
+    constexpr int kLA = la_of<W>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
@@ -412,7 +438,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         sm.filled[threadIdx.x] = 0;
     }
     if (threadIdx.x == 0) sm.zero = v4u{0u, 0u, 0u, 0u};
-    if (threadIdx.x < (WIDE ? 8 : BURG_NARROW_U))
+    if (threadIdx.x < (WIDE ? uw_of<W>() : BURG_NARROW_U))
         (WIDE ? &sm.zeros[0] : &sm.win[0][0][0])[threadIdx.x] = v4u{0u, 0u, 0u, 0u};
     // sweep: K / T trajectories of T steps (host guarantees <= kPipeSweepMax)
     const int nsw = SWEEP ? a.K / a.T : 1;

@@ -253,7 +253,9 @@ def main():
     res = {"source": "tools/isa_count.py (hipcc -O3 --offload-arch=gfx950 -save-temps of pipe.hip)",
            "issue_model": "4 cycles per instruction + 12 per fp64 transcendental (one wave per SIMD)"}
     for W, sweep in ((256, False), (16, True), (16, False)):
-        U = 8  # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U, 8 since round 3)
+        # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U): 16 for wide
+        # tiles of 128 and 256 columns, 8 otherwise (round 3)
+        U = 16 if W in (128, 256) else 8
         rr = hot_cycle(parse_blocks(kernel_body(asm, W, sweep)), U)
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
