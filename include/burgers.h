@@ -163,7 +163,10 @@ void burg_ctx_destroy(burg_ctx *ctx);
  *   inv_dx[nx]        = 1/dx_c              (make_ddx, C/hypernet2D.py:2414)
  *   inv_dy[ny_total]  = 1/dy_r
  *   src[nx]           = dt*0.02*exp(mu2*xc) (:2550)
- *   lbc[ny_total]     = 0.5*dt*mu1**2/dx[r] (:2553-2554, row-indexed quirk)  */
+ *   lbc[ny_total]     = 0.5*dt*mu1**2/dx[r] (:2553-2554, row-indexed quirk)
+ * BURG_EINVAL unless dt > 0 and every dt/4 * inv_dx[c], dt/4 * inv_dy[r] is in
+ * (0, 2^100) (the march's fast path relies on it; any physical grid and dt
+ * are far inside).  */
 int burg_set_problem(burg_ctx *ctx, const double *inv_dx, const double *inv_dy,
                      const double *src, const double *lbc, double dt);
 
