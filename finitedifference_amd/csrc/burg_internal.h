@@ -146,6 +146,7 @@ struct PipeArgs {
     const double *lbc_b;  // [K/T][ny] inlet term of trajectory j, this slab's rows
     int qbase;            // absolute step of local step 0, mod 2*kPipeR (sentinel colour)
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
+    int wg_cm;            // workgroup order: 1 column-major (tile row fastest), 0 row-major
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid
     unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)

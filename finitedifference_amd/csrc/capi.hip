@@ -529,6 +529,16 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.ntj = c->sp.ntj;
     a.ntiles = c->sp.ntiles;
     a.nwj = c->nwj;
+    {
+        // Column-major workgroup order where row-major would give each XCD
+        // (the dispatcher deals workgroup i to XCD i mod 8) whole column groups
+        // of tiles (nwj a multiple of 8): 8192 x 2048 slab 146 -> 169,
+        // 16384 x 2048 137 -> 152 Gcell-updates/s, 1024^2 sweep / trajectory
+        // +0.8 / +1.5 %; 4096^2 (nwj = 4) 0.4 % slower that way
+        // (profiles/r03/ab/wg_order.txt).  BURG_WG_MAP=0/1 forces an order.
+        const char *e = std::getenv("BURG_WG_MAP");
+        a.wg_cm = e ? (std::atoi(e) != 0) : (c->nwj % 8 == 0);
+    }
     a.spin_ticks = c->spin_ticks;
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
     a.err = c->d_err;

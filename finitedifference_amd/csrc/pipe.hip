@@ -380,7 +380,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
-    const int ti = wg / a.nwj, g = wg - ti * a.nwj;
+    // a.wg_cm (host: pipe_args): column-major, workgroup i -> tile row i % nti,
+    // so the dispatcher's XCD (i mod 8) is a tile-row class, not a column group
+    const int ti = a.wg_cm ? wg % a.nti : wg / a.nwj;
+    const int g = a.wg_cm ? wg / a.nti : wg - ti * a.nwj;
     const int tj0 = 4 * g;
     const int ntj = a.ntj;
     const int ny = a.cf.ny;
