@@ -8,7 +8,7 @@ mkdir -p $O
 rm -f $O/ab.txt
 X="--no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e --no-residual-check --steps 4 --warmup 1"
 for rep in 1 2; do
-for m in auto 0 1; do
+for m in ${MAPS:-auto 0 1}; do
   if [ $m = auto ]; then unset BURG_WG_MAP; else export BURG_WG_MAP=$m; fi
   for nx in 8192 16384; do
     timeout -k 10 200 python bench.py --nx $nx --rows-per-gpu 2048 $X > $O/s.json 2> $O/s.err || { tail -5 $O/s.err; exit 1; }
