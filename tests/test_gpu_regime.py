@@ -173,6 +173,27 @@ def test_chunked_ring_wrap_bitwise(gpu, orc, monkeypatch, nx, ny, W, T, chunk):
     assert np.array_equal(ctx.download(), ref2[T])
 
 
+@pytest.mark.parametrize("nx,ny,W,T", [(2048, 130, 64, 6), (512, 192, 16, 7), (2100, 100, 256, 5)])
+def test_workgroup_order_bitwise(gpu, orc, monkeypatch, nx, ny, W, T):
+    """Both workgroup orders of the pipe kernel (BURG_WG_MAP: 0 row-major, 1
+    column-major -- the planner's choice when a strip has a multiple of 8
+    workgroups, the per-GPU slabs of the N > 1 bench and the 1024^2 narrow
+    tiles) produce the oracle's trajectory bit for bit, from the planted w0
+    (slow path included); a ragged top strip and a partial last workgroup
+    (2100 / 256 = 9 tiles) included."""
+    P = _problem(orc, nx, ny)
+    w0 = planted_w0(nx, ny)
+    ref, _, _ = P.fom(w0, T)
+    for order in ("0", "1"):
+        monkeypatch.setenv("BURG_WG_MAP", order)
+        ctx = _ctx(nx, ny, engine="pipe", stream_w=W)
+        snaps, st, _, _ = ctx.run(w0, T)
+        assert st["stream_w"] == W
+        for j in range(T + 1):
+            assert np.array_equal(snaps[:, j], ref[j]), f"order {order} step {j}"
+        ctx.close()
+
+
 def test_trajectory_ring_not_stale_after_run(gpu, orc):
     """A ring re-allocated by burg_run after a trajectory must not be taken
     for a memory-capped one (ring_maxed was never cleared): the
