@@ -725,6 +725,10 @@ int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_o
         const long long v = std::atoll(e);
         if (v > 0) C = std::min(C, v);
     }
+    if (const char *e = std::getenv("BURG_RING_CAP")) {  // test knob: a ring of at most v steps
+        const long long v = std::atoll(e);
+        if (v > 0) C = std::min(C, v);
+    }
     const long long have_L = (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave));
     bool maxed = false;
     if (C * W + W + 96 > have_L && !(c->ring_maxed && have_L >= 2 * W + 96)) {
@@ -765,12 +769,21 @@ int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats 
     stream_stats_begin(c);
     CHK(launch_ring_load(stream_args(c, L, 0, 0), W, from_initial ? c->d_w0 : c->d_state[c->cur],
                          c->stream));
+    // A ring of fewer steps than the trajectory (capped by free memory: the
+    // 16384 x 2048 slab of the N = 8 bench) wraps INSIDE one launch, as
+    // stream_advance's two-step ring does: the states older than C steps are
+    // overwritten either way, and the wavefront's fill and drain (nx + rows
+    // diagonals, ~7 % of that slab's trajectory) are paid once, not per
+    // chunk.  BURG_STREAM_CHUNK (tests) still splits the launches.
+    long long Kmax = std::max<long long>(C, stream_max_steps(c));
+    if (const char *e = std::getenv("BURG_STREAM_CHUNK"))
+        if (std::atoll(e) > 0) Kmax = C;
     float ms = 0.f;
     long long origin = 0;
     int done = 0, last = 0;
     int64_t launches = 0;
     while (done < num_steps) {
-        const int K = (int)std::min<long long>(num_steps - done, C);
+        const int K = (int)std::min<long long>(num_steps - done, Kmax);
         if (int e = stream_launch(c, L, origin, K, &ms)) return e;
         origin = (origin + (long long)K * W) % L;
         done += K;

@@ -194,6 +194,29 @@ def test_workgroup_order_bitwise(gpu, orc, monkeypatch, nx, ny, W, T):
         ctx.close()
 
 
+@pytest.mark.parametrize("nx,ny,W,T,cap", [(2100, 64, 1024, 12, 5), (700, 200, 256, 11, 4),
+                                           (1000, 130, 128, 13, 3), (256, 128, 16, 13, 5)])
+def test_capped_ring_one_launch_bitwise(gpu, orc, monkeypatch, nx, ny, W, T, cap):
+    """A trajectory ring capped below the trajectory's length (BURG_RING_CAP
+    stands in for the free-memory cap of the 16384 x 2048 slab) wraps inside
+    ONE launch: burg_trajectory's final state bit-equal to the oracle from the
+    planted w0, and again when the trajectory continues over the same ring."""
+    monkeypatch.setenv("BURG_RING_CAP", str(cap))
+    P = _problem(orc, nx, ny)
+    w0 = planted_w0(nx, ny)
+    ref, _, _ = P.fom(w0, T)
+    ctx = _ctx(nx, ny, engine="pipe", stream_w=W)
+    ctx.upload(w0)
+    st = ctx.trajectory(T)
+    assert st["stream_w"] == W and st["stream_launches"] == 1
+    assert np.array_equal(ctx.download(), ref[T])
+    st = ctx.trajectory(T, from_initial=False)
+    assert st["stream_launches"] == 1
+    ref2, _, _ = P.fom(ref[T], T)
+    assert np.array_equal(ctx.download(), ref2[T])
+    ctx.close()
+
+
 def test_trajectory_ring_not_stale_after_run(gpu, orc):
     """A ring re-allocated by burg_run after a trajectory must not be taken
     for a memory-capped one (ring_maxed was never cleared): the
