@@ -100,6 +100,12 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #ifndef BURG_RING_AUX
 #define BURG_RING_AUX 16
 #endif
+// cache policy of the loader's ring reads (LDS-DMA): 18 = sc1 + nt, each
+// entry is read once (4096^2 49.0 -> 46.2 ms per trajectory against sc1
+// alone, profiles/r03/ab/ring_load_nt.txt)
+#ifndef BURG_LOAD_AUX
+#define BURG_LOAD_AUX 18
+#endif
 #ifndef BURG_NARROW_U
 #define BURG_NARROW_U 8
 #endif
@@ -636,7 +642,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
-                                                                 (unsigned)e * 1024u + lane * 16u, 0, 0, 16);
+                                                                 (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
                         e = e + 1 == L ? 0 : e + 1;
                         slot = slot + 1 == KWIN ? 0 : slot + 1;
                     }
