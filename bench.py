@@ -6,9 +6,12 @@
 
 Unit of work ("step"): ONE FOM TRAJECTORY = run_fom.main's time loop
 (inviscid_burgers_implicit2D, C/hypernet2D.py:72-131): T = 500 implicit time
-steps of the whole grid from w0 = 1 at mu = (5.19, 0.026), every intermediate
-state kept resident in HBM (the snapshot matrix, engine ring layout), solved
-exactly by the HIP march in ONE pipelined launch (burg_trajectory).
+steps of the whole grid from w0 = 1 at mu = (5.19, 0.026), solved exactly by
+the HIP march in ONE pipelined launch (burg_trajectory_ex), the snapshot
+matrix kept resident in HBM (engine ring layout): every state when the whole
+trajectory fits (N = 1, 4096^2: 134 GB), else every 10th state (--snap-every;
+the N > 1 slabs: 268 / 537 GB would be needed per GPU) -- config.snap_every /
+retained_states say which.
 --sweep N times the snapshot sweep over the first N training mu instead
 (burg_sweep; C/run_prom.py:59-71).
 
@@ -75,6 +78,12 @@ def parse():
                          "(get_snapshot_params); 1 = one trajectory at mu=(5.19, 0.026)")
     ap.add_argument("--time-steps", type=int, default=500,
                     help="implicit steps per trajectory (run_fom.py: 500)")
+    ap.add_argument("--snap-every", type=int, default=0,
+                    help="states kept in HBM per trajectory: every k-th (burg_trajectory_ex); "
+                         "0 = auto: every state when the whole trajectory fits in HBM (4096^2: "
+                         "134 GB), else every 10th (the 8192 x 2048 / 16384 x 2048 slabs)")
+    ap.add_argument("--no-alone", action="store_true",
+                    help="N > 1: skip per_gpu_alone (the per-GPU shape run as one rank first)")
     ap.add_argument("--nx", type=int, default=None,
                     help="row length (default by GPU count: 4096, 8192, 8192, 16384 for N = 1, 2, "
                          "4, 8)")
@@ -235,8 +244,9 @@ def end_to_end(nx=1024, T=500):
 
 def block_of(W):
     """Diagonals per readiness block of the pipe kernel (pipe.hip uw_of):
-    16 for wide tiles of 128 and 256 columns, 8 otherwise (round 3)."""
-    return 16 if W in (128, 256) else 8
+    16 for wide tiles of 128 ... 1024 columns (512, 1024 since round 4),
+    8 otherwise."""
+    return 16 if W >= 128 else 8
 
 
 def issue_roofline(kname, avg_ms, diagonals, isa_file, W, U=8, clock_ghz=None, clock_src=None):
@@ -405,7 +415,7 @@ def main():
             # the trajectory ring (134 GB at 4096^2 x 500 steps) is allocated
             # here, before the barrier: no rank's first launch waits on a
             # neighbour still allocating (the halo waits are bounded in time)
-            c.reserve(T)
+            c.reserve(T, snap_every=args.snap_every)
         return c
 
     def barrier():
@@ -425,7 +435,7 @@ def main():
                 return None
             try:
                 if nmu == 1:
-                    return c.trajectory(T)
+                    return c.trajectory(T, snap_every=args.snap_every)
                 return c.sweep(mus, T, keep_snaps=False)[1]
             except BurgersError as e:
                 err.append(e)
@@ -461,6 +471,14 @@ def main():
         return int(t.item())
 
     from finitedifference_amd._lib import BurgersError
+    alone = None
+    if world > 1 and nmu == 1 and not args.no_alone:
+        # the same per-GPU shape as ONE rank (no halo) on rank 0's GPU, before
+        # the collective run: the weak-scaling reference that separates the
+        # halo / ramp cost from the tile shape's own rate
+        if rank == 0:
+            alone = per_gpu_alone(nx, rows, dt, T, args, dev)
+        dist.barrier()
     ctx = setup()
     halo_fallback = None
     res, err = measure(ctx)
@@ -477,6 +495,8 @@ def main():
     if code:
         raise RuntimeError(f"rank {rank}: the timed run failed ({err or 'on another rank'})")
     elapsed, kern_ms, launches, st = res
+    # what the timed trajectories kept resident (before the residual check reuses the ring)
+    ret_first, ret_count, ret_stride = ctx.retained() if nmu == 1 else (0, 0, 0)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if rehearse else "cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -484,7 +504,7 @@ def main():
     check = None
     if not args.no_residual_check:
         check = residual_check(ctx, T, dist if world > 1 else None,
-                               None if rehearse or world == 1 else dev)
+                               None if rehearse or world == 1 else dev, args.snap_every)
     cells = nx * ny  # whole job
     value = cells * T * nmu * args.steps / elapsed / 1e6
 
@@ -536,6 +556,14 @@ def main():
                 "baseline_config": BASELINE_CONFIGS.get((nx, ny, world)),
                 "nx": nx, "ny": ny, "rows_per_gpu": rows, "time_steps": T, "dt": dt,
                 "trajectories_per_step": nmu,
+                "snap_every": ret_stride if nmu == 1 else None,
+                "retained_states": ret_count if nmu == 1 else None,
+                "retained_first_state": ret_first if nmu == 1 else None,
+                "retained_note": ("states kept in HBM per trajectory and GPU (burg_trajectory_ex): "
+                                  "every state while the whole trajectory fits, else every "
+                                  "snap_every-th in retained ring windows (no extra traffic); "
+                                  "the reference keeps every state in host memory"
+                                  if nmu == 1 else None),
                 "parallelism": f"row-slab x{world}",
                 "halo_ring": halo,
                 "halo_fallback": halo_fallback,
@@ -556,6 +584,9 @@ def main():
                 "traffic_source": tsrc,
             },
         }
+        if alone is not None:
+            out["per_gpu_alone"] = alone
+            out["weak_eff_same_shape"] = round(value / (world * alone["value"]), 4)
         if st["engine"] == 2:
             clk, csrc = read_clock(args.pmc_file, key)
             iss = issue_roofline(kname, avg_ms, T * nmu * st["stream_w"] + nx + rows,
@@ -582,10 +613,41 @@ def main():
         sys.exit(3)
 
 
+def per_gpu_alone(nx, rows, dt, T, args, dev):
+    """One rank's shape (nx x rows cells, the slab's cell size and dt) as a
+    single-domain context on `dev`: W untimed + min(K, 3) timed trajectories,
+    the same snap_every; Mcell-updates/s of one GPU with no halo."""
+    import torch
+    from finitedifference_amd.solver import FOMContext
+    c = FOMContext(nx, rows, device=dev, engine=args.engine, stream_w=args.stream_w)
+    c.set_problem(np.linspace(0, 100, nx + 1), np.linspace(0, 100.0 * rows / nx, rows + 1), dt, MU,
+                  allow_nonsquare=(nx != rows))
+    c.upload(np.ones(c.m))
+    c.reserve(T, snap_every=args.snap_every)
+    for _ in range(max(1, args.warmup)):
+        c.trajectory(T, snap_every=args.snap_every)
+    k = max(1, min(args.steps, 3))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kern = 0.0
+    for _ in range(k):
+        kern += c.trajectory(T, snap_every=args.snap_every)["loop_ms"]
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    f, n, stride = c.retained()
+    c.close()
+    return {"value": round(nx * rows * T * k / el / 1e6, 3), "unit": "Mcell-updates/s",
+            "shape": f"{nx}x{rows}", "trajectories": k,
+            "kernel_ms": round(kern / k, 3), "snap_every": stride, "retained_states": n,
+            "what": "the per-GPU shape of this line run as ONE rank (single domain, no halo) on "
+                    "rank 0's GPU before the collective run; weak_eff_same_shape = value / "
+                    "(n_gpus * this)"}
+
+
 RESIDUAL_TOL = 1e-13
 
 
-def residual_check(ctx, T, dist=None, device=None):
+def residual_check(ctx, T, dist=None, device=None, snap_every=1):
     """The run checks its own result: w_{T-1} and w_T of the bench's
     trajectory (burg_trajectory from w0 at mu = (5.19, 0.026)) are taken from
     two more launches, and the last step must solve the reference residual
@@ -595,11 +657,11 @@ def residual_check(ctx, T, dist=None, device=None):
     ratio (max over ranks)."""
     from finitedifference_amd.dist import slab_residual_norms
     if T >= 2:
-        ctx.trajectory(T - 1)
+        ctx.trajectory(T - 1, snap_every=snap_every)
         wpm = ctx.download()
     else:
         wpm = np.ones(ctx.m)  # the uploaded w0
-    ctx.trajectory(T)
+    ctx.trajectory(T, snap_every=snap_every)
     wT = ctx.download()
     n1, s1 = slab_residual_norms(ctx, wT, wpm, dist, device)
     n0, s0 = slab_residual_norms(ctx, wpm, wpm, dist, device)
@@ -647,11 +709,20 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
     iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 2 * nx, isa_file,
                          st["stream_w"], U=block_of(st["stream_w"]), clock_ghz=clk,
                          clock_src=csrc) if isa_file else None
+    # the narrow tiles keep the previous state in LDS: the bytes they move
+    # (PMC) are ~0.6 x the 32-B model's, so the fraction on measured traffic
+    # says how close to HBM they actually run
+    meas = (round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+            if isinstance(traffic, (int, float)) and traffic > 0 else None)
     return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"9-mu snapshot sweep x {T} steps",
             "issue_roofline": iss,
             "value": round(upd * steps / el / 1e6, 3), "unit": "Mcell-updates/s",
             "kernel": kname, "avg_launch_ms": round(ms, 4),
             "roofline_frac": round(gbs / HBM_PEAK_GBS, 5), "achieved_GBs": round(gbs, 1),
+            "roofline_frac_measured_traffic": meas,
+            "roofline_frac_note": "roofline_frac: 32 B per cell-update (SURVEY 8(d)) / kernel "
+                                  "time / 8 TB/s; _measured_traffic: PMC HBM bytes per launch "
+                                  "(traffic) / kernel time / 8 TB/s",
             "ieee_diagonals": st["ieee_diagonals"], "traffic": traffic, "traffic_source": tsrc}
 
 

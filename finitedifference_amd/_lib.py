@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -26,7 +26,8 @@ EXPORTS = (
     "burg_slab_connect", "burg_slab_verify", "burg_slab_halo_note", "burg_slab_halo_mode", "burg_ctx_destroy", "burg_set_problem", "burg_set_options",
     "burg_residual", "burg_slab_residual", "burg_jvp", "burg_block_solve", "burg_run", "burg_upload_state",
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
-    "burg_reserve_trajectory",
+    "burg_reserve_trajectory", "burg_trajectory_ex", "burg_reserve_trajectory_ex",
+    "burg_trajectory_plan", "burg_trajectory_retained", "burg_trajectory_copy",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
     "burg_pod", "burg_pod_rsvd", "burg_run_npy",
 )
@@ -134,6 +135,19 @@ def load(path=None):
             "burg_trajectory": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
                                                 ctypes.POINTER(BurgStats)]),
             "burg_reserve_trajectory": (ctypes.c_int, [_VP, ctypes.c_int]),
+            "burg_trajectory_ex": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.POINTER(BurgStats)]),
+            "burg_reserve_trajectory_ex": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int]),
+            "burg_trajectory_plan": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int,
+                                                     ctypes.POINTER(ctypes.c_int),
+                                                     ctypes.POINTER(ctypes.c_int64),
+                                                     ctypes.POINTER(ctypes.c_int64)]),
+            "burg_trajectory_retained": (ctypes.c_int, [_VP, ctypes.POINTER(ctypes.c_int64),
+                                                         ctypes.POINTER(ctypes.c_int64),
+                                                         ctypes.POINTER(ctypes.c_int)]),
+            "burg_trajectory_copy": (ctypes.c_int, [_VP, ctypes.c_int64, ctypes.c_int64,
+                                                     ctypes.c_void_p, ctypes.c_int64,
+                                                     ctypes.c_int]),
             "burg_set_engine": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
             "burg_kernel_bench": (ctypes.c_int, [_VP, ctypes.c_int, ctypes.c_int, _D]),
             "burg_ecsw_matrix": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int, _D, _D,

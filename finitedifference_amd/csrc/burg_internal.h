@@ -95,15 +95,46 @@ struct StreamPlan {
     int W, nti, ntj, ntiles, R;
 };
 
+// Where a tile's ring keeps diagonal s of a launch (s >= -W: the launch's
+// initial state sits at diagonals -W .. 62, state q >= 1 at diagonals
+// (q-1) W .. q W + 62 -- lane l, column c of state q at (q-1) W + c + l).
+//   * plain ring (k == 0): entry (origin + s) mod L;
+//   * retained windows (k >= 2, one launch from origin 0; the snap_every of
+//     burg_trajectory_ex): window j < n holds the
+//     W + 64 diagonals starting at ((j+1) k - 1) W -- every cell of state
+//     (j+1) k, which no later diagonal overwrites -- at entries base +
+//     j (W + 64) + offset; every other diagonal goes to a working ring of L
+//     entries whose position pauses inside the windows.  Each diagonal is
+//     still stored exactly once: keeping every k-th state costs no traffic.
+// Windows must not overlap (k W >= W + 64) and begin on block boundaries
+// (W + 64, k W and L multiples of the block).
+__host__ __device__ inline long long ring_pos(long long s, long long origin, long long L, int W,
+                                              int k, int n, long long base)
+{
+    if (k > 0) {
+        const long long r = s - (long long)(k - 1) * W;
+        if (r >= 0) {
+            const long long kw = (long long)k * W, j = r / kw, o = r - j * kw;
+            if (j < n && o < W + 64) return base + j * (W + 64) + o;
+            s -= (j < n ? j + 1 : n) * (long long)(W + 64);  // retained diagonals before s
+        }
+    }
+    const long long d = (origin + s) % L;
+    return d < 0 ? d + L : d;
+}
+
 struct StreamArgs {
     Coeffs cf;
     const d2 *colc;      // [ntj*W] {hx, src} per column
-    d2 *ring;            // [ntiles][L][64] state by diagonal
+    d2 *ring;            // [ntiles][Lt][64] state by diagonal
     d2 *wbox;            // [ntiles][R][64] west-edge mailboxes
     d2 *sbox;            // [ntiles][R][W]  south-edge mailboxes
     size_t wbox_bytes, sbox_bytes;
     long long origin;    // ring entry of diagonal 0
-    long long L;         // ring length (diagonals)
+    long long L;         // ring length (diagonals); the working ring with retained windows
+    long long Lt;        // entries per tile (>= L: + the retained windows)
+    int ret_k, ret_n;    // retained windows (ring_pos): snap_every, windows; 0: plain ring
+    long long ret_base;  // entry of window 0
     int K;               // time steps of this launch
     int flags;           // diagnostics only: bit 0 = ignore neighbours (wrong results)
     int nti, ntj, ntiles, R;
@@ -135,7 +166,10 @@ struct PipeArgs {
     d2 *halo_in;          // south inflow of the bottom strip (written by rank-1)
     d2 *halo_out;         // north outflow of the top strip (read by rank+1)
     size_t halo_bytes;
-    long long origin, L;  // ring entry of diagonal 0, ring length
+    long long origin, L;  // ring entry of diagonal 0, ring length (working ring: ring_pos)
+    long long Lt;         // ring entries per tile (>= L: + the retained windows)
+    int ret_k, ret_n;     // retained windows (ring_pos): snap_every, windows; 0: plain ring
+    long long ret_base;   // entry of window 0
     int K;                // steps of this launch
     // Parameter sweep (burg_sweep): the launch runs K / T trajectories of T
     // steps back to back, each from the initial state, trajectory j with
@@ -146,6 +180,11 @@ struct PipeArgs {
     const double *lbc_b;  // [K/T][ny] inlet term of trajectory j, this slab's rows
     int qbase;            // absolute step of local step 0, mod 2*kPipeR (sentinel colour)
     int nti, ntj, ntiles, nwj;  // tile grid; nwj = workgroups per strip
+    // side-by-side domains (burg_sweep at small grids): nd domains of nti_d
+    // strips (ny_d real rows) each, stacked; domain j reads column table
+    // colc + j * colc_dstride.  nd = 1: one domain, nti_d = nti, ny_d = cf.ny.
+    int nd, nti_d, ny_d;
+    size_t colc_dstride;
     int wg_cm;            // workgroup order: 1 column-major (tile row fastest), 0 row-major
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid

@@ -93,6 +93,26 @@ struct TraceRange {
 };
 #define BURG_TRACE(name) TraceRange burg_trace_range_(name)
 
+// The ring layout of a trajectory launch (ring_pos, burg_internal.h): a plain
+// ring of L entries from `origin`, or (k >= 2) a working ring of L entries plus
+// n retained windows of W + 64 entries from entry `base`; Lt entries per tile.
+struct TrajMap {
+    long long L = 0, origin = 0, Lt = 0, base = 0;
+    int k = 0, n = 0;
+};
+
+// What the last burg_trajectory_ex left resident (burg_trajectory_retained):
+// states first, first + stride, ... (count of them), read through `map`
+// (state q of the trajectory is state q - state0 of the map's launch); with
+// ret0 the trajectory's initial state is the copy d_ret0.
+struct TrajRecord {
+    bool valid = false;
+    TrajMap map;
+    int64_t T = 0, state0 = 0, first = 0, count = 0;
+    int stride = 1;
+    bool ret0 = false;
+};
+
 struct burg_ctx {
     int device = 0;
     int nx = 0, ny_total = 0, row0 = 0, nrows = 0;
@@ -160,6 +180,16 @@ struct burg_ctx {
     size_t halo_bytes = 0;
     bool halo_connected = false;
     bool slab_failed = false;        // a launch failed: refuse further launches (BURG_ESTATE)
+    int64_t launches = 0;            // march launches of this context (test hook)
+    // side-by-side domains (an internal sweep context, burg_sweep): bat_nd
+    // domains of bat_ny_d rows, each padded to whole strips; per-domain column
+    // tables bat_colc_stride apart (ov_colc)
+    int bat_nd = 1, bat_ny_d = 0;
+    size_t bat_colc_stride = 0;
+    double *d_halo_rows = nullptr;   // burg_slab_residual: the south halo rows of w, wp (4 nx)
+    TrajRecord tr;                   // the last trajectory's resident states
+    double *d_ret0 = nullptr;        // its initial state (retained windows: the working ring
+                                     // overwrites it)
     bool halo_out_resolved = false;  // producer: took the consumer's verdict (first launch)
     std::string halo_note;           // why a device ring was not used
 
@@ -468,6 +498,7 @@ int stream_setup(burg_ctx *c)
 
 int ensure_ring(burg_ctx *c, long long L)
 {
+    c->tr.valid = false;  // the caller overwrites the ring
     const size_t need = (size_t)c->sp.ntiles * (size_t)L * kWave;
     if (need <= c->ring_entries) return 0;
     dfree(c->d_ring);
@@ -478,9 +509,15 @@ int ensure_ring(burg_ctx *c, long long L)
     return 0;
 }
 
-StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
+StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K, const TrajMap *mp = nullptr)
 {
     StreamArgs a{};
+    a.Lt = (mp && mp->Lt >= L) ? mp->Lt : L;
+    if (mp && mp->k > 0) {
+        a.ret_k = mp->k;
+        a.ret_n = mp->n;
+        a.ret_base = mp->base;
+    }
     a.cf = c->cf;
     a.colc = c->d_colc;
     a.ring = c->d_ring;
@@ -505,9 +542,15 @@ StreamArgs stream_args(burg_ctx *c, long long L, long long origin, int K)
 // stay addressable by one buffer descriptor (< 2 GiB)
 int stream_max_steps(const burg_ctx *c) { return ((1 << 21) - 4096) / c->sp.W - 1; }
 
-PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
+PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const TrajMap *mp = nullptr)
 {
     PipeArgs a{};
+    a.Lt = (mp && mp->Lt >= L) ? mp->Lt : L;
+    if (mp && mp->k > 0) {
+        a.ret_k = mp->k;
+        a.ret_n = mp->n;
+        a.ret_base = mp->base;
+    }
     a.cf = c->cf;
     a.colc = c->d_colc;
     a.ring = c->d_ring;
@@ -529,6 +572,16 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     a.ntj = c->sp.ntj;
     a.ntiles = c->sp.ntiles;
     a.nwj = c->nwj;
+    a.nd = 1;
+    a.nti_d = c->sp.nti;
+    a.ny_d = c->nrows;
+    a.colc_dstride = 0;
+    if (c->bat_nd > 1) {
+        a.nd = c->bat_nd;
+        a.nti_d = c->sp.nti / c->bat_nd;
+        a.ny_d = c->bat_ny_d;
+        a.colc_dstride = c->bat_colc_stride;
+    }
     {
         // Column-major workgroup order where row-major would give each XCD
         // (the dispatcher deals workgroup i to XCD i mod 8) whole column groups
@@ -550,7 +603,8 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K)
     return a;
 }
 
-int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
+int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
+                  const TrajMap *mp = nullptr)
 {
     BURG_TRACE("march launch");
     const bool pipe = c->eng_eff == BURG_ENGINE_PIPE;
@@ -558,19 +612,42 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
         return fail(BURG_ESTATE, "a launch of this slab context failed earlier: its halo rings hold "
                                  "stale step colours, so every rank must destroy and recreate its "
                                  "context");
-    // test hook (BURG_TEST_FAIL_DEVICE_HALO=1): a launch with a device-memory
-    // halo ring fails as a stalled halo wait would, without launching --
-    // exercises the bench's fall-back to the host rings (tools/gpu_round.sh)
-    if (const char *e = std::getenv("BURG_TEST_FAIL_DEVICE_HALO"))
-        if (std::strcmp(e, "1") == 0 && (c->halo_in_mode == 2 || c->halo_out_mode == 2)) {
+    // test hook: a launch with a device-memory halo ring fails as a stalled
+    // halo wait would, without launching -- exercises the bench's fall-back to
+    // the host rings (tools/gpu_round.sh).  BURG_TEST_FAIL_DEVICE_HALO=1: every
+    // such launch; =R:K: only rank R's launch number K (0-based, counted per
+    // context) -- the other ranks then meet a neighbour that stopped, and
+    // their bounded waits give up on their own (tools/gpu_r4.sh rehearsal)
+    const int64_t launch_no = c->launches++;
+    if (const char *e = std::getenv("BURG_TEST_FAIL_DEVICE_HALO")) {
+        int hr = -1;
+        long long hk = -1;
+        const bool all = std::strcmp(e, "1") == 0;
+        const bool one = !all && std::sscanf(e, "%d:%lld", &hr, &hk) == 2 && hr == c->rank &&
+                         hk == launch_no;
+        if ((all || one) && (c->halo_in_mode == 2 || c->halo_out_mode == 2)) {
             c->slab_failed = true;
             return fail(BURG_EHIP, "pipe engine: a wait timed out (test hook "
-                                   "BURG_TEST_FAIL_DEVICE_HALO: device halo ring)");
+                                   "BURG_TEST_FAIL_DEVICE_HALO=%s: device halo ring)", e);
         }
+    }
+    // Every failure return from here on leaves a slab's halo rings (shared
+    // with its neighbours) in an unknown colour state: a world > 1 context
+    // then refuses further launches (not only on the kernel's own
+    // error word, also on a failed launch, event or copy)
+    struct SlabFailGuard {
+        burg_ctx *c;
+        bool ok = false;
+        ~SlabFailGuard()
+        {
+            if (!ok && c->world > 1) c->slab_failed = true;
+        }
+    } guard{c};
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
-        CHK(launch_pipe(pipe_args(c, L, origin, K), c->sp.W, c->stream));
+        CHK(launch_pipe(pipe_args(c, L, origin, K, mp), c->sp.W, c->stream));
     } else {
+        if (mp && mp->k > 0) return fail(BURG_EINVAL, "retained windows need the pipe engine");
         CHK(launch_stream(stream_args(c, L, origin, K), c->sp.W, c->stream));
     }
     HIPCHK(hipEventRecord(c->ev1, c->stream));
@@ -582,8 +659,7 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
     HIPCHK(hipMemcpy(err, c->d_err, sizeof err, hipMemcpyDeviceToHost));
     if (err[0]) {
         // a slab's halo rings (shared with its neighbours) cannot be reset by
-        // one rank alone: the context refuses further launches
-        if (c->world > 1) c->slab_failed = true;
+        // one rank alone: the context refuses further launches (the guard)
         // leave the mailboxes clean for the next launch
         (void)hipMemsetAsync(c->d_err, 0, sizeof err, c->stream);
         if (pipe) {
@@ -613,6 +689,7 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms)
                     err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W);
     }
     if (pipe) c->qbase = (int)((c->qbase + (long long)K) % (2 * kPipeR));
+    guard.ok = true;
     return 0;
 }
 
@@ -710,14 +787,30 @@ int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
     return 0;
 }
 
+// Entries per tile of a trajectory ring of L entries (the tile stride): the
+// HBM channel a ring entry lands on follows its address, and all tiles
+// write the same ring position at about the same time -- a stride that is a
+// multiple of a large power of two (a retained-window ring: Lw + n (W + 64) =
+// 2^8 x odd KB at 16384 x 2048) puts every tile's stream on the same
+// channels.  Default: an odd number of entries (1 KB each).  BURG_RING_PAD=n
+// (A/B knob): exactly n extra entries.
+long long ring_stride(long long L)
+{
+    static long long pad = -2;
+    if (pad == -2) {
+        pad = -1;
+        if (const char *e = std::getenv("BURG_RING_PAD")) pad = std::atoll(e);
+    }
+    if (pad >= 0) return L + pad;
+    return L | 1;
+}
+
 // The trajectory ring for num_steps: C steps per launch, L entries.  A ring
 // already sized to the memory limit is reused as it is: the next call would
 // only get the same size back, after a free and a fresh allocation of up to
 // ~240 GB (seconds per call at 8192^2).
-int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_out)
+int plain_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_out)
 {
-    if (int e = stream_setup(c)) return e;
-    if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
     const int W = c->sp.W;
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     long long C = std::min(num_steps, stream_max_steps(c));
@@ -731,69 +824,195 @@ int trajectory_ring(burg_ctx *c, int num_steps, long long *C_out, long long *L_o
     }
     const long long have_L = (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave));
     bool maxed = false;
-    if (C * W + W + 96 > have_L && !(c->ring_maxed && have_L >= 2 * W + 96)) {
+    const long long pad = ring_stride(0);  // (at most this many entries of stride padding)
+    if (ring_stride(C * W + W + 96) > have_L && !(c->ring_maxed && have_L >= 2 * W + 96 + pad)) {
         // need a (bigger) ring: size it against free memory
         dfree(c->d_ring);
         c->ring_entries = 0;
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
-        const long long Lmax = (long long)(freeb / 100 * 85 / per_entry);
+        const long long Lmax = (long long)(freeb / 100 * 85 / per_entry) - pad;
         const long long Cmem = (Lmax - W - 96) / W;
         maxed = Cmem < C;
         C = std::min<long long>(C, Cmem);
         if (C < 1) return fail(BURG_ENOMEM, "not enough device memory for a one-step ring");
     } else {
-        C = std::min<long long>(C, (have_L - W - 96) / W);
+        C = std::min<long long>(C, (have_L - pad - W - 96) / W);
         maxed = c->ring_maxed;
     }
     const long long L = C * W + W + 96;
-    if (int e = ensure_ring(c, L)) return e;
+    if (int e = ensure_ring(c, ring_stride(L))) return e;
     c->ring_maxed = maxed;
     *C_out = C;
     *L_out = L;
     return 0;
 }
 
-// One device-resident trajectory: num_steps steps from d_state[cur] in ONE
-// launch, every state kept in the ring (HBM) -- the reference's snapshot
-// matrix in ring layout (C/hypernet2D.py:89-126 keeps them all); the final
-// state becomes d_state[cur].  A trajectory whose ring does not fit in 85 % of
-// free HBM (or one descriptor) runs as several launches over a ring of C
-// steps, each launch continuing from the previous one's last states.
-int stream_trajectory(burg_ctx *c, int num_steps, bool from_initial, burg_stats *st)
+// Does the whole num_steps trajectory fit a plain ring (85 % of free HBM plus
+// the ring already held, one buffer descriptor)?
+bool plain_ring_fits(burg_ctx *c, int num_steps)
 {
+    const int W = c->sp.W;
+    if (num_steps > stream_max_steps(c)) return false;
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    size_t freeb = 0, totalb = 0;
+    if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) return false;
+    const size_t need = (size_t)((long long)num_steps * W + W + 96) * per_entry;
+    const size_t have = c->ring_entries * sizeof(d2);
+    return need <= have || need <= (freeb + have) / 100 * 85;
+}
+
+// snap_every <= 0 ("auto"): every state when the whole trajectory fits a
+// plain ring, else every 10th
+int resolve_snap_every(burg_ctx *c, int num_steps, int snap_every)
+{
+    if (snap_every > 0) return snap_every;
+    return plain_ring_fits(c, num_steps) ? 1 : 10;
+}
+
+// The ring of a trajectory keeping every snap_every-th state (DESIGN.md
+// section 4.1d).  snap_every = 1: the plain ring (every state while it fits;
+// capped by free HBM it keeps the last C).  snap_every = k >= 2 on the pipe
+// engine: a working ring of 2W + 128 entries plus num_steps / k retained
+// windows of W + 64 entries (ring_pos) -- every k-th state survives the whole
+// launch at no extra traffic.  Narrow tiles whose windows would overlap (k W <
+// W + 64) and the streaming engine keep every state (a plain ring, which must
+// then hold the whole trajectory).
+int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, long long *C_out,
+                    int *k_out = nullptr)
+{
+    if (int e = stream_setup(c)) return e;
+    if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
+    const int W = c->sp.W;
+    const int k = resolve_snap_every(c, num_steps, snap_every);
+    if (k_out) *k_out = k;
+    *mp = TrajMap{};
+    if (k >= 2 && c->eng_eff == BURG_ENGINE_PIPE && (long long)k * W >= W + 64) {
+        const int n = num_steps / k;
+        const long long Lw = 2LL * W + 128;  // a multiple of every block length
+        const long long Lt = ring_stride(Lw + (long long)n * (W + 64));
+        if (Lt >= (1LL << 21))
+            return fail(BURG_ESHAPE, "%d retained states of %d-wide tiles exceed one buffer "
+                        "descriptor per tile (2 GiB); raise snap_every", n, W);
+        const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+        const size_t need = (size_t)Lt * per_entry, have = c->ring_entries * sizeof(d2);
+        if (need > have) {
+            dfree(c->d_ring);
+            c->ring_entries = 0;
+            size_t freeb = 0, totalb = 0;
+            HIPCHK(hipMemGetInfo(&freeb, &totalb));
+            if (need + c->m() * sizeof(double) > freeb / 100 * 85)
+                return fail(BURG_ENOMEM, "%d retained states (%.1f GB) do not fit in HBM; raise "
+                            "snap_every", n, (double)need / 1e9);
+        }
+        if (int e = ensure_ring(c, Lt)) return e;
+        if (!c->d_ret0)
+            if (int e = dalloc(&c->d_ret0, c->m())) return e;
+        mp->L = Lw;
+        mp->origin = 0;
+        mp->Lt = Lt;
+        mp->base = Lw;
+        mp->k = k;
+        mp->n = n;
+        *C_out = num_steps;
+        return 0;
+    }
     long long C = 0, L = 0;
-    if (int e = trajectory_ring(c, num_steps, &C, &L)) return e;
+    if (int e = plain_ring(c, num_steps, &C, &L)) return e;
+    if (k >= 2 && C < num_steps)
+        return fail(BURG_ENOMEM, "snap_every=%d on %d-wide tiles keeps every state, and the "
+                    "%d-step trajectory does not fit in HBM", k, W, num_steps);
+    mp->L = L;
+    mp->Lt = std::min<long long>(ring_stride(L),
+                                 (long long)(c->ring_entries / (c->sp.ntiles * (size_t)kWave)));
+    mp->k = 0;
+    mp->n = 0;
+    *C_out = C;
+    return 0;
+}
+
+// One device-resident trajectory: num_steps steps from d_state[cur] (or the
+// uploaded initial state) in ONE launch; the final state becomes
+// d_state[cur].  The states kept in HBM (burg_trajectory_retained, copied out
+// by burg_trajectory_copy):
+//   * snap_every = 1: every state, in the ring (the reference's snapshot
+//     matrix in ring layout, C/hypernet2D.py:89-126 keeps them all); a ring
+//     that does not fit in 85 % of free HBM holds C < num_steps steps and
+//     wraps INSIDE the launch -- the last C + 1 states stay, the older ones
+//     are overwritten;
+//   * snap_every = k >= 2: states 0, k, 2k, ... in retained windows
+//     (trajectory_ring), whatever the grid size;
+//   * snap_every <= 0: 1 if the whole trajectory fits, else 10.
+// Only a trajectory longer than one buffer descriptor can address
+// (stream_max_steps) or BURG_STREAM_CHUNK (tests) splits a plain-ring
+// trajectory into several launches, each continuing from the previous one's
+// last states; the retained states are then those of the last launch.
+int stream_trajectory(burg_ctx *c, int num_steps, int snap_every, bool from_initial,
+                      burg_stats *st)
+{
+    TrajMap mp;
+    long long C = 0;
+    int k = 1;
+    if (int e = trajectory_ring(c, num_steps, snap_every, &mp, &C, &k)) return e;
     const int W = c->sp.W;
     if (from_initial && !c->d_w0) return fail(BURG_ESTATE, "no uploaded initial state");
+    const double *start = from_initial ? c->d_w0 : c->d_state[c->cur];
     stream_stats_begin(c);
-    CHK(launch_ring_load(stream_args(c, L, 0, 0), W, from_initial ? c->d_w0 : c->d_state[c->cur],
-                         c->stream));
-    // A ring of fewer steps than the trajectory (capped by free memory: the
-    // 16384 x 2048 slab of the N = 8 bench) wraps INSIDE one launch, as
-    // stream_advance's two-step ring does: the states older than C steps are
-    // overwritten either way, and the wavefront's fill and drain (nx + rows
-    // diagonals, ~7 % of that slab's trajectory) are paid once, not per
-    // chunk.  BURG_STREAM_CHUNK (tests) still splits the launches.
+    CHK(launch_ring_load(stream_args(c, mp.L, 0, 0, &mp), W, start, c->stream));
+    if (mp.k > 0)
+        HIPCHK(hipMemcpyAsync(c->d_ret0, start, c->m() * sizeof(double), hipMemcpyDeviceToDevice,
+                              c->stream));
+    // A plain ring of fewer steps than the trajectory (capped by free memory)
+    // wraps INSIDE one launch, as stream_advance's two-step ring does: the
+    // states older than C steps are overwritten either way, and the
+    // wavefront's fill and drain (nx + rows diagonals, ~7 % of a 16384 x 2048
+    // slab's trajectory) are paid once, not per chunk.
     long long Kmax = std::max<long long>(C, stream_max_steps(c));
+    if (mp.k > 0) Kmax = num_steps;  // retained windows: one launch (the map is per launch)
     if (const char *e = std::getenv("BURG_STREAM_CHUNK"))
-        if (std::atoll(e) > 0) Kmax = C;
+        if (std::atoll(e) > 0 && mp.k == 0) Kmax = C;
     float ms = 0.f;
     long long origin = 0;
     int done = 0, last = 0;
     int64_t launches = 0;
     while (done < num_steps) {
         const int K = (int)std::min<long long>(num_steps - done, Kmax);
-        if (int e = stream_launch(c, L, origin, K, &ms)) return e;
-        origin = (origin + (long long)K * W) % L;
+        if (int e = stream_launch(c, mp.L, origin, K, &ms, &mp)) return e;
+        origin = (origin + (long long)K * W) % mp.L;
         done += K;
         last = K;
         ++launches;
     }
-    const long long o_last = ((origin - (long long)last * W) % L + L) % L;
-    CHK(launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1, c->d_state[c->cur ^ 1],
-                            1, c->stream));
+    const long long o_last = ((origin - (long long)last * W) % mp.L + mp.L) % mp.L;
+    mp.origin = o_last;
+    CHK(launch_ring_extract(stream_args(c, mp.L, o_last, 0, &mp), W, last, 1, 1,
+                            c->d_state[c->cur ^ 1], 1, c->stream));
     c->cur ^= 1;
+    // what stays resident
+    TrajRecord &tr = c->tr;
+    tr = TrajRecord{};
+    tr.map = mp;
+    tr.T = num_steps;
+    tr.state0 = num_steps - last;
+    if (mp.k > 0) {
+        tr.first = 0;
+        tr.count = mp.n + 1;
+        tr.stride = mp.k;
+        tr.ret0 = true;
+    } else {
+        // state r of the last launch occupies its diagonals (r-1) W .. r W + 62;
+        // it is intact unless a later diagonal (up to last W + 62) reused an
+        // entry, i.e. while (r-1) W + L > last W + 62
+        // (snap_every k >= 2 on a plain ring -- narrow tiles whose windows
+        // would overlap -- keeps every state: report the multiples of k)
+        long long r0 = 0;
+        while (r0 <= last && (r0 - 1) * W + mp.L <= (long long)last * W + 62) ++r0;
+        const int64_t f = (tr.state0 + r0 + k - 1) / k * k;
+        tr.first = f;
+        tr.count = f <= num_steps ? (num_steps - f) / k + 1 : 0;
+        tr.stride = k;
+    }
+    tr.valid = true;
     if (int e = stream_stats_end(c, st, num_steps, launches)) return e;
     if (st) {
         st->loop_ms = ms;
@@ -810,6 +1029,7 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
                int snap_every, burg_stats *st, int32_t *step_iters, double *step_rel)
 {
     if (int e = stream_setup(c)) return e;
+    c->tr.valid = false;  // the ring is overwritten
     const int W = c->sp.W;
     const size_t m = c->m(), bytes = m * sizeof(double);
     size_t freeb = 0, totalb = 0;
@@ -1282,6 +1502,8 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_x);
     dfree(c->d_partials);
     dfree(c->d_sumsq);
+    dfree(c->d_halo_rows);
+    dfree(c->d_ret0);
     stream_free(c);
     if (c->halo_out_ipc) (void)hipIpcCloseMemHandle(c->halo_out_ipc);
     if (c->halo_in_ring) (void)hipFree(c->halo_in_ring);
@@ -1407,11 +1629,16 @@ int burg_slab_residual(burg_ctx *c, const double *w, const double *wp, const dou
     const size_t bytes = c->m() * sizeof(double), hb = 2 * (size_t)c->nx * sizeof(double);
     HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->d_d, wp, bytes, hipMemcpyHostToDevice, c->stream));
-    double *d_halo = nullptr;
+    // the halo rows go to a scratch buffer kept by the context (allocated on
+    // first use: no hipMalloc / hipFree -- a device-wide sync -- per call)
+    const double *d_halo = nullptr;
     if (halo_w) {
-        if (int e = dalloc(&d_halo, 4 * (size_t)c->nx)) return e;
-        HIPCHK(hipMemcpyAsync(d_halo, halo_w, hb, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(d_halo + 2 * c->nx, halo_wp, hb, hipMemcpyHostToDevice, c->stream));
+        if (!c->d_halo_rows)
+            if (int e = dalloc(&c->d_halo_rows, 4 * (size_t)c->nx)) return e;
+        HIPCHK(hipMemcpyAsync(c->d_halo_rows, halo_w, hb, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->d_halo_rows + 2 * c->nx, halo_wp, hb, hipMemcpyHostToDevice,
+                              c->stream));
+        d_halo = c->d_halo_rows;
     }
     int rc = launch_residual(c->cf, c->d_x, c->d_d, c->d_r, c->d_partials, c->d_sumsq, d_halo,
                              d_halo ? d_halo + 2 * c->nx : nullptr, c->stream);
@@ -1421,7 +1648,6 @@ int burg_slab_residual(burg_ctx *c, const double *w, const double *wp, const dou
          hipMemcpyAsync(&s, c->d_sumsq, sizeof s, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess))
         rc = -3;
-    dfree(d_halo);
     if (rc) return fail(BURG_EHIP, "slab residual failed: %s", hipGetErrorString(hipGetLastError()));
     if (sumsq) *sumsq = s;
     return BURG_OK;
@@ -1558,26 +1784,147 @@ int burg_advance(burg_ctx *c, int num_steps, int solver, burg_stats *st)
     return BURG_OK;
 }
 
-int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st)
+int burg_trajectory_ex(burg_ctx *c, int num_steps, int snap_every, int from_initial,
+                       burg_stats *st)
 {
     BURG_TRACE("burg_trajectory");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (c->engine == BURG_ENGINE_TILES)
         return fail(BURG_EINVAL, "burg_trajectory runs on the stream/pipe engines");
-    return stream_trajectory(c, num_steps, from_initial != 0, st);
+    return stream_trajectory(c, num_steps, snap_every, from_initial != 0, st);
 }
 
-int burg_reserve_trajectory(burg_ctx *c, int num_steps)
+int burg_trajectory(burg_ctx *c, int num_steps, int from_initial, burg_stats *st)
+{
+    return burg_trajectory_ex(c, num_steps, 1, from_initial, st);
+}
+
+int burg_reserve_trajectory_ex(burg_ctx *c, int num_steps, int snap_every)
 {
     BURG_TRACE("burg_reserve_trajectory");
     if (int e = check_ready(c)) return e;
     if (c->engine == BURG_ENGINE_TILES)
         return fail(BURG_EINVAL, "burg_reserve_trajectory serves the stream/pipe engines");
-    long long C = 0, L = 0;
-    if (int e = trajectory_ring(c, num_steps, &C, &L)) return e;
+    TrajMap mp;
+    long long C = 0;
+    if (int e = trajectory_ring(c, num_steps, snap_every, &mp, &C)) return e;
     HIPCHK(hipStreamSynchronize(c->stream));
     return BURG_OK;
+}
+
+int burg_reserve_trajectory(burg_ctx *c, int num_steps)
+{
+    return burg_reserve_trajectory_ex(c, num_steps, 1);
+}
+
+int burg_trajectory_plan(burg_ctx *c, int num_steps, int snap_every, int *snap_every_out,
+                         int64_t *retained_states, int64_t *ring_bytes)
+{
+    if (int e = check_ready(c)) return e;
+    if (c->engine == BURG_ENGINE_TILES)
+        return fail(BURG_EINVAL, "burg_trajectory_plan serves the stream/pipe engines");
+    if (num_steps < 1) return fail(BURG_EINVAL, "num_steps must be >= 1");
+    if (int e = stream_setup(c)) return e;
+    const int k = resolve_snap_every(c, num_steps, snap_every);
+    const int W = c->sp.W;
+    const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
+    int64_t nret = 0, bytes = 0;
+    if (k >= 2 && c->eng_eff == BURG_ENGINE_PIPE && (long long)k * W >= W + 64) {
+        nret = num_steps / k + 1;
+        bytes = (int64_t)((2LL * W + 128 + (long long)(num_steps / k) * (W + 64)) * per_entry);
+    } else if (plain_ring_fits(c, num_steps)) {
+        nret = k >= 2 ? num_steps / k + 1 : num_steps + 1;
+        bytes = (int64_t)(((long long)num_steps * W + W + 96) * per_entry);
+    } else {
+        nret = -1;  // a capped plain ring: the last C + 1 states (known after the run)
+    }
+    if (snap_every_out) *snap_every_out = k;
+    if (retained_states) *retained_states = nret;
+    if (ring_bytes) *ring_bytes = bytes;
+    return BURG_OK;
+}
+
+int burg_trajectory_retained(burg_ctx *c, int64_t *first_state, int64_t *count, int *stride)
+{
+    if (!c) return fail(BURG_EINVAL, "null context");
+    if (!c->tr.valid) return fail(BURG_ESTATE, "no trajectory resident (burg_trajectory_ex)");
+    if (first_state) *first_state = c->tr.first;
+    if (count) *count = c->tr.count;
+    if (stride) *stride = c->tr.stride;
+    return BURG_OK;
+}
+
+static int check_device_ptr(const burg_ctx *c, const void *p, const char *what);
+
+// Columns col0 .. col0 + ncols - 1 of the resident trajectory (state
+// first + j * stride in column j) into the C-order (2n x ld_out) matrix `out`
+// at column offsets 0 .. ncols - 1: host memory (staged, pinned when it can
+// be registered) or, with out_on_device, device memory of this GPU.
+int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, int64_t ld_out,
+                         int out_on_device)
+{
+    BURG_TRACE("burg_trajectory_copy");
+    if (int e = check_ready(c)) return e;
+    const TrajRecord &tr = c->tr;
+    if (!tr.valid) return fail(BURG_ESTATE, "no trajectory resident (burg_trajectory_ex)");
+    if (!out) return fail(BURG_EINVAL, "null output");
+    if (col0 < 0 || ncols < 0 || col0 + ncols > tr.count)
+        return fail(BURG_EINVAL, "columns [%lld, %lld) outside the %lld retained", (long long)col0,
+                    (long long)(col0 + ncols), (long long)tr.count);
+    if (ld_out < ncols || ld_out > INT32_MAX) return fail(BURG_EINVAL, "ld_out=%lld", (long long)ld_out);
+    if (ncols == 0) return BURG_OK;
+    if (out_on_device)
+        if (int e = check_device_ptr(c, out, "out")) return e;
+    const int W = c->sp.W;
+    const size_t m = c->m();
+    const StreamArgs ra = stream_args(c, tr.map.L, tr.map.origin, 0, &tr.map);
+    // state q of the trajectory -> (relative state of the map's launch)
+    auto rel = [&](int64_t j) { return tr.first + j * tr.stride - tr.state0; };
+    int64_t j = col0;
+    const int64_t j1 = col0 + ncols;
+    int rc = BURG_OK;
+    double *d_tr = nullptr;
+    bool registered = false;
+    int S = 0;
+    if (!out_on_device) {
+        size_t freeb = 0, totalb = 0;
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        S = (int)std::min<int64_t>(ncols, 64);
+        while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
+        if (int e = dalloc(&d_tr, (size_t)S * m)) return e;
+        registered = hipHostRegister(out, m * (size_t)ld_out * sizeof(double),
+                                     hipHostRegisterDefault) == hipSuccess;
+        (void)hipGetLastError();
+    }
+    while (j < j1 && rc == BURG_OK) {
+        double *dst = out_on_device ? out + (j - col0) : d_tr;
+        const int ldo = out_on_device ? (int)ld_out : S;
+        int n = 0;
+        if (tr.ret0 && rel(j) == 0) {
+            // the initial state: its copy (the working ring has moved on)
+            const double *p0 = c->d_ret0;
+            if (launch_transpose(&p0, 1, m, dst, ldo, c->stream)) rc = fail(BURG_EHIP, "column copy failed");
+            n = 1;
+        } else {
+            n = (int)std::min<int64_t>(j1 - j, out_on_device ? INT32_MAX : S);
+            if (launch_ring_extract(ra, W, (int)rel(j), tr.stride, n, dst, ldo, c->stream))
+                rc = fail(BURG_EHIP, "ring extract launch failed");
+        }
+        if (rc == BURG_OK && !out_on_device &&
+            hipMemcpy2DAsync(out + (j - col0), (size_t)ld_out * sizeof(double), d_tr,
+                             (size_t)S * sizeof(double), (size_t)n * sizeof(double), m,
+                             hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
+        if (rc == BURG_OK && !out_on_device && hipStreamSynchronize(c->stream) != hipSuccess)
+            rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
+        j += n;
+    }
+    if (rc == BURG_OK && hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
+    if (registered) (void)hipHostUnregister(out);
+    dfree(d_tr);
+    return rc;
 }
 
 int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,

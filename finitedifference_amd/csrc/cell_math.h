@@ -130,20 +130,24 @@ struct MarchCell {
         double s, nu, nv;
         if constexpr (FAST) {
             // The fast window: Cu, Cv POSITIVE with magnitude in [2^-900,
-            // 2^900), div2_normal's exact range.  Then q = 0.25 + h_x Cu + h_y Cv
-            // is >= 0.25 (h_x, h_y > 0) and finite (h_x, h_y < 2^100, checked by
-            // burg_set_problem), inside sqrt_normal's exact range, and s =
-            // 0.5 + sqrt(q) >= 1: no test of q is needed.  Tested on the high
-            // words: less 123 << 20, a positive operand's word is below
-            // 1800 << 20 iff its biased exponent is in [123, 1922] (a smaller
-            // one borrows past the top, a negative one has the top bit set).
-            // Zeros, negatives, denormals, Inf and NaN take the IEEE path
-            // (which reports a NaN): the reference regime's velocities are
-            // positive, and a negative Cu / Cv is still computed exactly.  Two
-            // subtracts, a max and a compare.
+            // 2^798), inside div2_normal's exact range.  Then q = 0.25 + h_x Cu
+            // + h_y Cv is >= 0.25 (h_x, h_y > 0) and below 0.25 + 2^100 2^798
+            // 2 < 2^900 (h_x, h_y < 2^100, checked by burg_set_problem), i.e.
+            // inside sqrt_normal's exact range [2^-900, 2^900), and s = 0.5 +
+            // sqrt(q) is in [1, 2^450]: no test of q is needed (round 4: the
+            // window's top was 2^900, which let q reach 2^1001 for h near
+            // 2^100 -- outside the range the sequences are verified on).
+            // Tested on the high words: less 123 << 20, a positive operand's
+            // word is below 1698 << 20 iff its biased exponent is in [123,
+            // 1820] (a smaller one borrows past the top, a negative one has
+            // the top bit set).  Zeros, negatives, denormals, Inf, NaN and
+            // operands >= 2^798 take the IEEE path (which reports a NaN): the
+            // reference regime's velocities are positive and O(1), and a
+            // negative Cu / Cv is still computed exactly.  Two subtracts, a
+            // max and a compare.
             const unsigned xu = (unsigned)__double2hiint(cu) - (123u << 20);
             const unsigned xv = (unsigned)__double2hiint(cv) - (123u << 20);
-            range_ok = max(xu, xv) < (1800u << 20);
+            range_ok = max(xu, xv) < (1698u << 20);
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

@@ -63,15 +63,17 @@
 // (s_memrealtime): a wave that gives up sets the error word and the LDS abort
 // flag, and the launch drains.
 #include <climits>
+#include <cstddef>
 #include <type_traits>
 
 #include "burg_internal.h"
 #include "cell_math.h"
 
 // pipe_narrow.hip includes this file with BURG_PIPE_NARROW_TU = 1: it
-// compiles the narrow-tile kernels (W = 8, 16) with the default machine
-// scheduler, this unit the wide ones with max-ilp (profiles/r02/sched/: each
-// strategy wins on its own width class)
+// compiles the narrow-tile kernels (W = 8, 16) in their own unit, this one the
+// wide ones; both units are built with LLVM's max-ilp machine scheduler (the
+// Makefile: narrow +1.2 % with 8-diagonal blocks, round 3; round 2's 4-diagonal
+// blocks had preferred the default scheduler, profiles/r02/sched/)
 #ifndef BURG_PIPE_NARROW_TU
 #define BURG_PIPE_NARROW_TU 0
 #endif
@@ -133,17 +135,36 @@ constexpr int la_of();
 #endif
 template <int W>
 constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
-// Blocks of 16 diagonals for W = 128, 256 (round 3; window 32 diagonals, LDS
-// rings of 2 steps between the workgroup's waves -- the room for it; the LDS
-// DMA reaches past 64 KB, tools/probes/dma_high_probe.hip): the block head is
-// paid once per 16 diagonals -- 4096^2 53.0 -> 49.0 ms per trajectory
-// (profiles/r03/ab/wide_u16.txt).  W = 512, 1024 keep blocks of 8 (their
-// column tables leave no room for a 32-diagonal window).
+// Blocks of 16 diagonals for W = 128 ... 1024 (round 3 for 128, 256; window
+// 32 diagonals, LDS rings of 2 steps between the workgroup's waves -- the
+// room for it; the LDS DMA reaches past 64 KB, tools/probes/
+// dma_high_probe.hip): the block head is paid once per 16 diagonals --
+// 4096^2 53.0 -> 49.0 ms per trajectory (profiles/r03/ab/wide_u16.txt).
+// W = 512, 1024 (round 4): their full column tables (8 / 16 KB per wave)
+// left no room for the 32-diagonal window, so they keep a rolling window of
+// the last kCCW columns instead (ccw_of), refilled by the loader wave.
 #ifndef BURG_WIDE_U16
 #define BURG_WIDE_U16 1
 #endif
+#ifndef BURG_WIDE_U16_512
+#define BURG_WIDE_U16_512 1
+#endif
 template <int W>
-constexpr bool u16_of() { return BURG_WIDE_U16 && !two_per_cu<W>() && (W == 128 || W == 256); }
+constexpr bool u16_of()
+{
+    return BURG_WIDE_U16 && !two_per_cu<W>() &&
+           (W == 128 || W == 256 || (BURG_WIDE_U16_512 && (W == 512 || W == 1024)));
+}
+// Rolling column table (W >= 512 with blocks of 16): slot t mod kCCW holds
+// {hx, src} of local time t's column while lanes can need it.  A block at
+// diagonal sb reads t in [sb - 63, sb + U); the loader writes the columns of
+// the blocks it fills, t in [prog + U, prog + KWIN) (prog = the compute
+// wave's block): 95 < kCCW apart, so no live slot is overwritten.
+constexpr int kCCW = 128;
+template <int W>
+constexpr bool ccw_of() { return u16_of<W>() && W >= 512; }
+template <int W>
+constexpr int ccn_of() { return ccw_of<W>() ? kCCW : W; }  // column-table slots (before padding)
 template <int W>
 constexpr int win_of() { return two_per_cu<W>() ? 12 : u16_of<W>() ? 32 : W >= 1024 ? 16 : BURG_KWIN; }  // window (diagonals)
 template <int W>
@@ -279,6 +300,36 @@ __device__ __forceinline__ long long now_rt() { return (long long)__builtin_amdg
 // through a VGPR select and a vector compare)
 __device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
 
+// Walk of a tile's diagonals one block of U at a time through the retained
+// windows of ring_pos (burg_internal.h; a.ret_k > 0): entry of the block's
+// first diagonal, in scalar registers, advanced per block without divisions.
+// The windows, the working ring's wrap (L a multiple of U, origin 0) and the
+// blocks all start on multiples of U, so a block's U diagonals are U
+// consecutive entries.  s0: first diagonal of the walk, <= 0.
+struct RetCursor {
+    int j, o;    // window index, diagonal - (window j's first diagonal)
+    unsigned w;  // working-ring position of the next diagonal outside a window
+    __device__ void init(const PipeArgs &a, int W, int s0)
+    {
+        j = 0;
+        o = s0 - (a.ret_k - 1) * W;
+        long long e = (a.origin + s0) % a.L;
+        w = (unsigned)(e < 0 ? e + a.L : e);
+    }
+    __device__ unsigned next(const PipeArgs &a, int W, int U)
+    {
+        const bool inw = (o >= 0) & (o < W + 64) & (j < a.ret_n);
+        const unsigned e = inw ? (unsigned)a.ret_base + (unsigned)(j * (W + 64) + o) : w;
+        if (!inw) w = w + U >= (unsigned)a.L ? w + U - (unsigned)a.L : w + U;
+        o += U;
+        if (o == a.ret_k * W) {
+            o = 0;
+            ++j;
+        }
+        return e;
+    }
+};
+
 
 // LDS accesses that must not be cached in registers or merged (polled / handed
 // off between waves).  Explicit address space 3: a volatile access through a
@@ -319,8 +370,10 @@ template <int W, bool SWEEP>
 struct PipeLds {
     static constexpr bool WIDE = is_wide<W>();
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
-    // wide: previous states by diagonal, filled by LDS-DMA -- first in the
-    // image: the DMA's LDS address comes from M0[15:0] (the 64 KB below 2^16)
+    // wide: previous states by diagonal, filled by LDS-DMA (M0 base + 16 B
+    // per lane) -- first in the image; the DMA reaches every byte of the
+    // CU's LDS, not only the 64 KB below 2^16 (tools/probes/dma_high_probe.hip
+    // writes and checks 0 .. 160 KB: profiles/r04/dma_high_probe.txt)
     // (narrow tiles: unused by the window; its 8 entries hold the zero south
     // inflow of a boundary strip, read by block offsets -- see zeros)
     v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : BURG_NARROW_U];
@@ -331,7 +384,7 @@ struct PipeLds {
     // per wave: {hx, src} of the tile's columns, + the first kPad again, so a
     // steady block's lane reads base + u unwrapped (W = 8: no steady blocks)
     static constexpr int kPad = W == 8 ? 0 : (WIDE ? uw_of<W>() : BURG_NARROW_U);
-    v4u cc[4][W + kPad];
+    v4u cc[4][ccn_of<W>() + kPad];  // (W >= 512: the rolling window, ccw_of)
     v4u ewe[3][rl_of<W>()][kWave]; // wave k -> k+1 east outflow, by step slot and row
     v4u inw[rl_of<W>()][kWave];    // west inflow of wave 0 (comm wave deposits)
     v4u ins[4][ni_of<W, SWEEP>()];  // south inflow of each wave, by diagonal (comm wave deposits)
@@ -366,6 +419,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     constexpr int kThreads = threads_of<W>();
     static_assert(win_of<W>() % uw_of<W>() == 0, "the window holds whole blocks");
     static_assert(sizeof(PipeLds<W, SWEEP>) <= 160 * 1024, "LDS image exceeds the CU's 160 KiB");
+    // the LDS-DMA window sits at the image's start and ends below the range
+    // the probe verified (tools/probes/dma_high_probe.hip: 0 .. 160 KB)
+    using Img = PipeLds<W, SWEEP>;
+    static_assert(offsetof(Img, win) == 0 && sizeof(Img::win) <= 160 * 1024,
+                  "LDS-DMA window outside the probed range");
+    static_assert(!(u16_of<W>() && two_per_cu<W>()), "blocks of 16 need the whole CU's LDS");
     constexpr bool WIDE = is_wide<W>();
     // three narrow W=8 workgroups per CU: room for 8 slab processes sharing one
     // GPU (the 750^2 C5 case, tests/test_gpu_parity.py) with all grids resident
@@ -393,13 +452,23 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     const int tj0 = 4 * g;
     const int ntj = a.ntj;
     const int ny = a.cf.ny;
-    const int nrow = min(kWave, ny - ti * kWave);
+    // Side-by-side domains (a.nd > 1: burg_sweep's small-grid mode, DESIGN.md
+    // section 4.1e): the strips are a.nd independent domains of a.nti_d
+    // strips each, stacked (a domain's rows padded to whole strips; the
+    // coefficient rows of cf are tiled the same way).  A domain's first strip
+    // sees the boundary in the south, its last strip is partial and has no
+    // north neighbour, and its columns read the domain's own table (mu2).
+    const int dom = a.nd > 1 ? ti / a.nti_d : 0;
+    const int tl = ti - dom * a.nti_d;  // strip within the domain
+    const int ny_d = a.nd > 1 ? a.ny_d : ny;
+    const d2 *const colc_d = a.colc + (size_t)dom * a.colc_dstride;
+    const int nrow = min(kWave, ny_d - tl * kWave);
     const int top = nrow - 1;
     const int nval = min(4, ntj - tj0);  // valid tiles (waves) of this workgroup
     const int K = a.K;
     const int KW = K * W;
-    const bool south_dev = ti > 0, south_host = ti == 0 && a.halo_in != nullptr;
-    const bool north_dev = ti + 1 < a.nti, north_host = ti + 1 == a.nti && a.halo_out != nullptr;
+    const bool south_dev = tl > 0, south_host = tl == 0 && a.halo_in != nullptr;
+    const bool north_dev = tl + 1 < a.nti_d, north_host = tl + 1 == a.nti_d && a.halo_out != nullptr;
     const int hcols = a.cf.nx;  // halo ring row length (granules): real columns only
 
     // ---- residency census: every workgroup must be on the GPU at once
@@ -467,17 +536,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
-        for (int c = lane; c < W + PipeLds<W, SWEEP>::kPad; c += kWave) {
-            const d2 v = a.colc[(size_t)(tj0 + wave) * W + (c & (W - 1))];
+        // (the rolling window starts with the columns of t = 0 .. kCCW - 1)
+        for (int c = lane; c < ccn_of<W>() + PipeLds<W, SWEEP>::kPad; c += kWave) {
+            const d2 v = colc_d[(size_t)(tj0 + wave) * W + (c & (ccn_of<W>() - 1))];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
         if constexpr (!WIDE) {
             // state 0 of the lane's column c sits at diagonal c + lane - W (slot (c + lane) mod W)
-            const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
-                                                     (size_t)a.L * kWave * 16);
+            const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.Lt * kWave,
+                                                     (size_t)a.Lt * kWave * 16);
             for (int c = 0; c < W; ++c) {
-                long long e = (a.origin + c + lane - W) % a.L;
-                e = e < 0 ? e + a.L : e;
+                const long long e = ring_pos(c + lane - W, a.origin, a.L, W, a.ret_k, a.ret_n, a.ret_base);
                 const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
                 sm.st[wave][(c + lane) & (W - 1)][lane] = x0;
                 if constexpr (SWEEP) sm.st0[wave][(c + lane) & (W - 1)][lane] = x0;
@@ -624,6 +693,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const int total = (KW + kWave - 1 + U - 1) / U * U;
         const long long L = a.L;
         int nf[4] = {0, 0, 0, 0};
+        // retained windows: per wave, the walk of the entries it reads
+        // (diagonal nf - W), block by block
+        const bool ret = a.ret_k > 0;
+        RetCursor rc[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) rc[k].init(a, W, -W);
         long long t_prog = now_rt();
         for (;;) {
             bool left = false;
@@ -635,10 +710,30 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
                 if (nf[k] < lim) {
                     const __amdgpu_buffer_rsrc_t ring =
-                        rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * L * kWave, (size_t)L * kWave * 16);
-                    long long e = (a.origin + nf[k] - W) % L;
-                    e = e < 0 ? e + L : e;
+                        rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
+                    long long e;
+                    if (ret) {
+                        e = rc[k].next(a, W, U);  // (a window's entries lie past L: no wrap below)
+                    } else {
+                        e = (a.origin + nf[k] - W) % L;
+                        e = e < 0 ? e + L : e;
+                    }
                     int slot = nf[k] % KWIN;
+                    if constexpr (ccw_of<W>()) {
+                        // the block's U columns into the rolling table (slot
+                        // t mod kCCW, and its padding copy for the first U
+                        // slots; else the same slot again): 2 DMAs of U lanes,
+                        // issued before the window rows, landed by the same
+                        // waits (kLoadsPerBlock per block)
+                        const __amdgpu_buffer_rsrc_t colc = rsrc(colc_d + (size_t)(tj0 + k) * W, (size_t)W * 16);
+                        const int sl = nf[k] & (kCCW - 1);
+                        const unsigned co = (unsigned)((nf[k] + lane) & (W - 1)) * 16u;
+                        if (lane < U) {
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl], 16, co, 0, 0, 0);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl == 0 ? kCCW : sl], 16,
+                                                                     co, 0, 0, 0);
+                        }
+                    }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
@@ -653,8 +748,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             }
             const int nb = got[0] + got[1] + got[2] + got[3];
             if (nb) {
-                // wave k's rows have landed once at most U x (blocks issued
+                // wave k's rows have landed once at most NB x (blocks issued
                 // after it) loads are outstanding
+                constexpr int NB = U + (ccw_of<W>() ? 2 : 0);  // loads per block
                 int after = nb;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -662,9 +758,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     --after;
                     switch (after) {
                     case 0: wait_vmcnt<0>(); break;
-                    case 1: wait_vmcnt<U>(); break;
-                    case 2: wait_vmcnt<2 * U>(); break;
-                    default: wait_vmcnt<3 * U>(); break;
+                    case 1: wait_vmcnt<NB>(); break;
+                    case 2: wait_vmcnt<2 * NB>(); break;
+                    default: wait_vmcnt<3 * NB>(); break;
                     }
                     if (lane == 0) lds_sti(&sm.filled[k], nf[k]);
                 }
@@ -717,8 +813,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     typedef __attribute__((address_space(3))) const double lds_f64;
     lds_f64 *src_cur = (lds_f64 *)&sm.srcb[0][k][0];
     lds_f64 *src_nxt = (lds_f64 *)&sm.srcb[min(1, nsw - 1)][k][0];
-    const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.L * kWave,
-                                             (size_t)a.L * kWave * 16);
+    const __amdgpu_buffer_rsrc_t ring = rsrc(a.ring + (size_t)tile * a.Lt * kWave,
+                                             (size_t)a.Lt * kWave * 16);
     const __amdgpu_buffer_rsrc_t wbox = rsrc(a.wbox, a.wbox_bytes);
     // north outflow target: the north tile's south box, or the halo ring
     const __amdgpu_buffer_rsrc_t nrs = north_host ? rsrc(a.halo_out, a.halo_bytes)
@@ -736,6 +832,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     LDS v4u *const my_st0 = &sm.st0[k][0][0];
     const unsigned Lu = (unsigned)a.L;  // < 2^21 entries (one descriptor)
     unsigned pw = (unsigned)a.origin;
+    // retained windows (a.ret_k > 0): the ring entry of each block's first
+    // diagonal comes from the walk (set at the block start)
+    const bool ret = a.ret_k > 0;
+    RetCursor rcur;
+    rcur.init(a, W, 0);
     const v4u lempty = lds_empty_g();
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
@@ -815,7 +916,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.src = 0.0;
             in.xs = lds_ld(&sm.win[k][s % KWIN][lane]);
         }
-        in.cs = cc_ld(&sm.cc[k][c]);
+        in.cs = cc_ld(&sm.cc[k][t & (ccn_of<W>() - 1)]);  // (= c unless ccw_of)
         if constexpr (EDGE) in.gw = lds_ld(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.zero);
         else in.gw = v4u{0u, 0u, 0u, 0u};
         in.gs = lds_ld((has_south & (STEADY || s < KW)) ? &sm.ins[k][s & (kNI - 1)] : &sm.zero);
@@ -837,7 +938,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // starts at a multiple of U, so sb + u does not wrap)
         if constexpr (WIDE) b.wb = &sm.win[k][sb % KWIN][lane];
         else b.wb = (LDS v4u *)&my_st[(sb & (W - 1)) * kWave + lane];
-        b.cb = &sm.cc[k][(sb - lane) & (W - 1)];
+        b.cb = &sm.cc[k][(sb - lane) & (ccn_of<W>() - 1)];
         b.ib = has_south ? &sm.ins[k][sb & (kNI - 1)] : WIDE ? &sm.zeros[0] : &sm.win[0][0][0];
         b.c0 = (sb - lane) & (W - 1);
         b.sr = src_cur + b.c0;  // (padded row: + u does not wrap)
@@ -1221,6 +1322,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (waited) wait_ticks += __builtin_amdgcn_s_memtime() - c0;
             if (aborted) break;
         }
+        // (retained windows: the block's ring entries are consecutive and
+        // never wrap; plain ring: wrap checked below)
+        if (ret) pw = rcur.next(a, W, U);
+        const bool pw_nowrap = ret | (pw + U <= Lu);
         const int sm_ = sb & (W - 1);
         const int tt0 = sb - top, ct0 = tt0 & (W - 1);  // the top lane at the block start
         // (narrow tiles: the top lane's column may wrap to the next step
@@ -1232,7 +1337,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // run steady-edge blocks too; sweeps only where no lane is in the
         // first step of its next trajectory (that step reads the initial state)
         // (bitwise, not short-circuit: scalar ops and one branch, not a chain)
-        bool steady = (nrow == kWave) & (sb >= kWave) & (sb + U <= KW) & (pw + U <= Lu) &
+        bool steady = (nrow == kWave) & (sb >= kWave) & (sb + U <= KW) & pw_nowrap &
                       ((!WIDE & north_dev) | (ct0 + U <= min(W, ncol_real)));
         if constexpr (SWEEP)
             steady = steady & !any_lane(((sb + U - 1 - lane) >> LW) >= qn);

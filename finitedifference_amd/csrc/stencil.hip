@@ -7,6 +7,8 @@
 //                   of the reference's snaps matrix (:89-90, :126)
 // Op order of residual/jvp mirrors oracle/burgers_oracle.c (compiled with
 // -ffp-contract=off on both sides), so GPU == oracle bit for bit.
+#include <cstdlib>
+
 #include "burg_internal.h"
 
 namespace burg {
@@ -36,7 +38,7 @@ __device__ __forceinline__ double wave_shr1(double old0, double x)
 
 // Sum of squares of the cells this block owns, tree-reduced in a fixed
 // order (deterministic).
-__device__ __forceinline__ void block_sumsq(double x, double *partials)
+__device__ __forceinline__ void block_sumsq(double x, double *dst)
 {
     __shared__ double red[kBlock];
     red[threadIdx.x] = x;
@@ -45,7 +47,7 @@ __device__ __forceinline__ void block_sumsq(double x, double *partials)
         if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partials[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+    if (threadIdx.x == 0) *dst = red[0];
 }
 
 // rows per workgroup: enough workgroups to fill the chip (>= 2048), at
@@ -58,20 +60,43 @@ __host__ __device__ inline int stencil_rows(int nx, int ny)
     return rows;
 }
 
+// Which (column block, row block) workgroup `id` of the 1-D grid owns.  XCD:
+// the dispatcher deals workgroups round-robin to the 8 XCDs (id mod 8 share
+// one, MI355X_MICROARCH.md section "Workgroup dispatch"); the bijective
+// remap gives each XCD a contiguous band of blocks in row-major order, so a
+// block's west neighbour runs beside it and its south neighbour just before
+// it on the SAME XCD -- their halo lines (the west column, the south row) are
+// then still in that XCD's L2 instead of re-fetched from beyond it.
+template <bool XCD>
+__device__ __forceinline__ void block_of(int nbx, int nb, int &bx, int &by)
+{
+    int id = blockIdx.x;
+    if constexpr (XCD) {
+        const int q = nb / 8, r = nb % 8, x = id % 8;
+        id = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + id / 8;
+    }
+    by = id / nbx;
+    bx = id - by * nbx;
+}
+
 // halo_w / halo_wp: [u row | v row] of the row below this slab (nullptr =
-// domain boundary).
+// domain boundary).  PF: the next row's loads are issued before the current
+// row's arithmetic (two rows of loads in flight per lane).
+template <bool XCD, bool PF>
 __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const double *__restrict__ w,
                                                           const double *__restrict__ wp,
                                                           double *__restrict__ res,
                                                           double *__restrict__ partials,
                                                           const double *__restrict__ halo_w,
                                                           const double *__restrict__ halo_wp,
-                                                          int rows)
+                                                          int rows, int nbx, int nb)
 {
+    int bx, by;
+    block_of<XCD>(nbx, nb, bx, by);
     const int nx = cf.nx, ny = cf.ny;
     const size_t n = (size_t)nx * ny;
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    const int r0 = blockIdx.y * rows;
+    const int c = bx * kBlock + threadIdx.x;
+    const int r0 = by * rows;
     const int r1 = min(ny, r0 + rows);
     const bool colok = c < nx;
     const int cc = colok ? c : nx - 1;  // padding lanes mirror a real column, store nothing
@@ -84,6 +109,7 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
     const double axw = a * idxw;
     const double srcc = cf.src[cc];
     const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
+    const bool lw = lane0 && west;
 
     // south carry: Sv, Suv of the row below r0 and a*inv_dy of that row
     bool has_s = false;
@@ -101,14 +127,23 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
         SuvS = (0.5 * uS) * vS + (0.5 * upS) * vpS;
         has_s = true;
     }
+    // the row's loads (own cell; lane 0 also its west cell)
+    double nu = 0.0, nv = 0.0, nup = 0.0, nvp = 0.0, wu = 0.0, wv = 0.0, wup = 0.0, wvp = 0.0;
+    auto load_row = [&](int r) {
+        const size_t i = (size_t)r * nx + cc;
+        nu = u[i], nv = v[i], nup = up[i], nvp = vp[i];
+        if (lw) wu = u[i - 1], wv = v[i - 1], wup = up[i - 1], wvp = vp[i - 1];
+    };
+    if (PF && r0 < r1) load_row(r0);
     double sq = 0.0;
     for (int r = r0; r < r1; ++r) {
         const size_t i = (size_t)r * nx + cc;
-        const double ui = u[i], vi = v[i], upi = up[i], vpi = vp[i];
+        if (!PF) load_row(r);
+        const double ui = nu, vi = nv, upi = nup, vpi = nvp;
+        const double uj = wu, vj = wv, upj = wup, vpj = wvp;
+        if (PF && r + 1 < r1) load_row(r + 1);
         double SuW0 = 0.0, SuvW0 = 0.0;
-        if (lane0 && west) {
-            const size_t j = i - 1;
-            const double uj = u[j], vj = v[j], upj = up[j], vpj = vp[j];
+        if (lw) {
             SuW0 = 0.5 * (uj * uj) + 0.5 * (upj * upj);
             SuvW0 = (0.5 * uj) * vj + (0.5 * upj) * vpj;
         }
@@ -145,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
         ays = ay;
         has_s = true;
     }
-    block_sumsq(sq, partials);
+    block_sumsq(sq, partials + (size_t)by * nbx + bx);
 }
 
 __global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double *partials, int np,
@@ -166,14 +201,18 @@ __global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double *part
 // J(w) x: per cell the terms t1 = (ax u) xu, t2 = (0.5 ay) m, t3 = (ay v) xv,
 // t4 = (0.5 ax) m with m = v xu + u xv; the west cell's t1, t4 and the
 // south cell's t2, t3 enter with a minus sign (exact_jac2D, :2627-2656).
+template <bool XCD, bool PF>
 __global__ __launch_bounds__(kBlock) void jvp_kernel(Coeffs cf, const double *__restrict__ w,
                                                      const double *__restrict__ x,
-                                                     double *__restrict__ y, int rows)
+                                                     double *__restrict__ y, int rows, int nbx,
+                                                     int nb)
 {
+    int bx, by;
+    block_of<XCD>(nbx, nb, bx, by);
     const int nx = cf.nx, ny = cf.ny;
     const size_t n = (size_t)nx * ny;
-    const int c = blockIdx.x * kBlock + threadIdx.x;
-    const int r0 = blockIdx.y * rows;
+    const int c = bx * kBlock + threadIdx.x;
+    const int r0 = by * rows;
     const int r1 = min(ny, r0 + rows);
     const bool colok = c < nx;
     const int cc = colok ? c : nx - 1;
@@ -183,6 +222,7 @@ __global__ __launch_bounds__(kBlock) void jvp_kernel(Coeffs cf, const double *__
     const double ax = a * cf.inv_dx[cc];
     const double axw = west ? a * cf.inv_dx[cc - 1] : 0.0;
     const double *u = w, *v = w + n, *xu = x, *xv = x + n;
+    const bool lw = lane0 && west;
 
     bool has_s = false;
     double t2S = 0.0, t3S = 0.0;
@@ -194,14 +234,23 @@ __global__ __launch_bounds__(kBlock) void jvp_kernel(Coeffs cf, const double *__
         t3S = ays * v[j] * xv[j];
         has_s = true;
     }
+    double nu = 0.0, nv = 0.0, nxu = 0.0, nxv = 0.0, wu = 0.0, wv = 0.0, wxu = 0.0, wxv = 0.0;
+    auto load_row = [&](int r) {
+        const size_t i = (size_t)r * nx + cc;
+        nu = u[i], nv = v[i], nxu = xu[i], nxv = xv[i];
+        if (lw) wu = u[i - 1], wv = v[i - 1], wxu = xu[i - 1], wxv = xv[i - 1];
+    };
+    if (PF && r0 < r1) load_row(r0);
     for (int r = r0; r < r1; ++r) {
         const size_t i = (size_t)r * nx + cc;
-        const double ui = u[i], vi = v[i], xui = xu[i], xvi = xv[i];
+        if (!PF) load_row(r);
+        const double ui = nu, vi = nv, xui = nxu, xvi = nxv;
+        const double uj = wu, vj = wv, xuj = wxu, xvj = wxv;
+        if (PF && r + 1 < r1) load_row(r + 1);
         double t1W0 = 0.0, t4W0 = 0.0;
-        if (lane0 && west) {
-            const size_t j = i - 1;
-            const double mW = v[j] * xu[j] + u[j] * xv[j];
-            t1W0 = axw * u[j] * xu[j];
+        if (lw) {
+            const double mW = vj * xuj + uj * xvj;
+            t1W0 = axw * uj * xuj;
             t4W0 = 0.5 * axw * mW;
         }
         const double ay = a * cf.inv_dy[r];
@@ -270,14 +319,35 @@ int residual_partials_count(const Coeffs &cf)
     return ((cf.nx + kBlock - 1) / kBlock) * ((cf.ny + rows - 1) / rows);
 }
 
+// Stencil variant (A/B knob BURG_STENCIL, bits: 1 XCD-aware block order, 2
+// next-row prefetch; default kStencilDefault).  Every variant computes the
+// same cells with the same op order: the results are bit-identical.
+#ifndef BURG_STENCIL_DEFAULT
+#define BURG_STENCIL_DEFAULT 3
+#endif
+int stencil_variant()
+{
+    static int v = -1;
+    if (v < 0) {
+        v = BURG_STENCIL_DEFAULT;
+        if (const char *e = std::getenv("BURG_STENCIL")) v = std::atoi(e) & 3;
+    }
+    return v;
+}
+
 int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
                     double *partials, double *sumsq, const double *halo_w,
                     const double *halo_wp, hipStream_t st)
 {
     const int nb = residual_partials_count(cf);
     const int rows = stencil_rows(cf.nx, cf.ny);
-    const dim3 grid((cf.nx + kBlock - 1) / kBlock, (cf.ny + rows - 1) / rows);
-    residual_kernel<<<grid, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows);
+    const int nbx = (cf.nx + kBlock - 1) / kBlock;
+    switch (stencil_variant()) {
+    case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    }
     if (sumsq) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
@@ -285,8 +355,14 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
 int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y, hipStream_t st)
 {
     const int rows = stencil_rows(cf.nx, cf.ny);
-    const dim3 grid((cf.nx + kBlock - 1) / kBlock, (cf.ny + rows - 1) / rows);
-    jvp_kernel<<<grid, kBlock, 0, st>>>(cf, w, x, y, rows);
+    const int nbx = (cf.nx + kBlock - 1) / kBlock;
+    const int nb = nbx * ((cf.ny + rows - 1) / rows);
+    switch (stencil_variant()) {
+    case 0: jvp_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    case 1: jvp_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    case 2: jvp_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    default: jvp_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

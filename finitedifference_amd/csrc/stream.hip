@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
 
     // the tile's ring (L entries of 64 x 16 B) in HBM
     const __amdgpu_buffer_rsrc_t ring = __builtin_amdgcn_make_buffer_rsrc(
-        a.ring + (size_t)tile * a.L * kWave, 0, (int)(a.L * kWave * 16), 0x00020000);
+        a.ring + (size_t)tile * a.Lt * kWave, 0, (int)(a.Lt * kWave * 16), 0x00020000);
     const unsigned lane16 = lane * 16u;
     const __amdgpu_buffer_rsrc_t wbox =
         __builtin_amdgcn_make_buffer_rsrc(a.wbox, 0, (int)a.wbox_bytes, 0x00020000);
@@ -412,12 +412,11 @@ __global__ void fill_sent_kernel(d2 *p, size_t n)
 }
 
 // entry of state k (k >= 0) of local cell (lane, cl) of a tile
-__device__ __forceinline__ long long ring_entry(long long origin, long long L, int W, int k, int cl,
-                                                int lane)
+// ring entry of state k (0: the launch's initial state), column cl, lane
+__device__ __forceinline__ long long ring_entry(const StreamArgs &a, int W, int k, int cl, int lane)
 {
-    long long d = (long long)(k - 1) * W + cl + lane + origin;
-    d %= L;
-    return d < 0 ? d + L : d;
+    return ring_pos((long long)(k - 1) * W + cl + lane, a.origin, a.L, W, a.ret_k, a.ret_n,
+                    a.ret_base);
 }
 
 // C-order state w (u plane | v plane) -> ring entries of state 0.
@@ -438,7 +437,7 @@ __global__ void ring_load_kernel(StreamArgs a, int W, const double *w)
         const size_t j = (size_t)row * a.cf.nx + col;
         v = d2{w[j], w[n + j]};
     }
-    a.ring[((size_t)tile * a.L + ring_entry(a.origin, a.L, W, 0, cl, lane)) * kWave + lane] = v;
+    a.ring[((size_t)tile * a.Lt + ring_entry(a, W, 0, cl, lane)) * kWave + lane] = v;
 }
 
 // Snapshot extraction: out[e * ldo + j] = element e of state (k0 + j*kstep),
@@ -455,9 +454,7 @@ __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int 
     const int ti = row / kWave, lane = row - ti * kWave;
     const int tj = col / W, cl = col - tj * W;
     const int tile = ti * a.ntj + tj;
-    const d2 v = a.ring[((size_t)tile * a.L +
-                         ring_entry(a.origin, a.L, W, k0 + j * kstep, cl, lane)) *
-                            kWave +
+    const d2 v = a.ring[((size_t)tile * a.Lt + ring_entry(a, W, k0 + j * kstep, cl, lane)) * kWave +
                         lane];
     out[cell * ldo + j] = v.x;
     out[(n + cell) * ldo + j] = v.y;
@@ -482,8 +479,7 @@ __global__ void ring_extract_rows_kernel(StreamArgs a, int W, size_t e0, size_t 
     const int ti = row / kWave, lane = row - ti * kWave;
     const int tj = col / W, cl = col - tj * W;
     const int tile = ti * a.ntj + tj;
-    const d2 v = a.ring[((size_t)tile * a.L + ring_entry(a.origin, a.L, W, k0 + j * kstep, cl, lane)) *
-                            kWave +
+    const d2 v = a.ring[((size_t)tile * a.Lt + ring_entry(a, W, k0 + j * kstep, cl, lane)) * kWave +
                         lane];
     out[idx] = vplane ? v.y : v.x;
 }

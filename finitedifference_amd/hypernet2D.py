@@ -88,10 +88,11 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     (C/hypernet2D.py:72-131) on an MI355X.
 
     solver="march" (default) solves each implicit step exactly with the
-    closed-form upwind march, by default on the streaming engine (all steps
-    in one pipelined launch, bitwise the sequential march; engine="tiles"
-    selects the per-step block-Jacobi tile engine, tuned by tile_w / tol /
-    par_passes); solver="newton" runs the reference algorithm
+    closed-form upwind march, by default on the pipe engine (engine="pipe":
+    all steps in one pipelined launch, bitwise the sequential march;
+    engine="stream" the streaming engine it grew from, engine="tiles" the
+    per-step block-Jacobi tile engine, tuned by tile_w / tol / par_passes);
+    solver="newton" runs the reference algorithm
     (newton_raphson, max_its=100, relnorm_cutoff=1e-12, exact block solve).
     Both return the reference's snapshot matrix.  verbose=1 (default) prints
     what the reference prints, unchanged: the header line, then per step

@@ -198,20 +198,65 @@ class FOMContext:
         _lib.check(self._L.burg_download_state(self._h, _lib.dptr(w)))
         return w
 
-    def reserve(self, num_steps):
-        """Allocate the tiling, mailboxes and HBM ring trajectory(num_steps)
-        needs, without launching (burg_reserve_trajectory): multi-GPU ranks
-        call it before the barrier that precedes their first launch."""
-        _lib.check(self._L.burg_reserve_trajectory(self._h, int(num_steps)))
+    def reserve(self, num_steps, snap_every=1):
+        """Allocate the tiling, mailboxes and HBM ring trajectory(num_steps,
+        snap_every=...) needs, without launching (burg_reserve_trajectory_ex):
+        multi-GPU ranks call it before the barrier that precedes their first
+        launch."""
+        _lib.check(self._L.burg_reserve_trajectory_ex(self._h, int(num_steps), int(snap_every)))
 
-    def trajectory(self, num_steps, from_initial=True):
+    def trajectory(self, num_steps, from_initial=True, snap_every=1):
         """num_steps steps in one launch from the uploaded initial state (or,
-        from_initial=False, from the resident state), every state kept in HBM;
-        returns stats (loop_ms = the launch's device time)."""
+        from_initial=False, from the resident state); returns stats (loop_ms =
+        the launch's device time).  The states kept in HBM
+        (burg_trajectory_ex): snap_every=1 every state while they fit (a ring
+        capped by free HBM keeps the last ones), snap_every=k states 0, k, 2k,
+        ..., snap_every=0 auto (1 if the whole trajectory fits, else 10); see
+        retained() and trajectory_snaps()."""
         st = _lib.BurgStats()
-        _lib.check(self._L.burg_trajectory(self._h, int(num_steps), 1 if from_initial else 0,
-                                           ctypes.byref(st)))
+        _lib.check(self._L.burg_trajectory_ex(self._h, int(num_steps), int(snap_every),
+                                              1 if from_initial else 0, ctypes.byref(st)))
         return st.as_dict()
+
+    def trajectory_plan(self, num_steps, snap_every=1):
+        """(resolved snap_every, retained states or -1 for a capped ring, ring
+        bytes) of trajectory(num_steps, snap_every=...), without allocating."""
+        k, n, b = ctypes.c_int(), ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(self._L.burg_trajectory_plan(self._h, int(num_steps), int(snap_every),
+                                                ctypes.byref(k), ctypes.byref(n), ctypes.byref(b)))
+        return k.value, n.value, b.value
+
+    def retained(self):
+        """(first_state, count, stride): the states the last trajectory() keeps
+        resident are first_state + j * stride, j < count."""
+        f, n, k = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int()
+        _lib.check(self._L.burg_trajectory_retained(self._h, ctypes.byref(f), ctypes.byref(n),
+                                                    ctypes.byref(k)))
+        return f.value, n.value, k.value
+
+    def trajectory_snaps(self, col0=0, ncols=None, out=None):
+        """Retained columns col0 .. col0 + ncols - 1 of the last trajectory()
+        as a C-order (2n, ncols) snapshot matrix (the reference's layout,
+        C/hypernet2D.py:89-90,126): a new numpy array, `out` (numpy, written
+        in place), or a contiguous float64 torch tensor on this context's GPU
+        (burg_trajectory_copy on the device, no host round trip)."""
+        first, count, stride = self.retained()
+        ncols = count - col0 if ncols is None else int(ncols)
+        if out is not None and not isinstance(out, np.ndarray):
+            import torch
+            dev = torch.device("cuda", self.device)
+            if (out.dtype != torch.float64 or out.device != dev or not out.is_contiguous()
+                    or out.dim() != 2 or out.shape[0] != self.m or out.shape[1] < ncols):
+                raise ValueError(f"out must be a contiguous float64 ({self.m}, >= {ncols}) tensor "
+                                 f"on {dev}")
+            torch.cuda.current_stream(dev).synchronize()
+            _lib.check(self._L.burg_trajectory_copy(self._h, int(col0), ncols, out.data_ptr(),
+                                                    int(out.shape[1]), 1))
+            return out
+        snaps = _out_array(out, self.m, ncols)
+        _lib.check(self._L.burg_trajectory_copy(self._h, int(col0), ncols,
+                                                snaps.ctypes.data_as(ctypes.c_void_p), ncols, 0))
+        return snaps
 
     def sweep(self, mus, num_steps, w0=None, keep_snaps=True, snap_every=1, outs=None):
         """Parameter sweep (burg_sweep): one trajectory of num_steps steps per

@@ -51,7 +51,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 12
+#define BURG_ABI_VERSION 13
 
 enum burg_status {
     BURG_OK = 0,
@@ -235,20 +235,52 @@ int burg_download_state(burg_ctx *ctx, double *w);
  * burg_upload_state first. */
 int burg_kernel_bench(burg_ctx *ctx, int which, int reps, double *avg_ms);
 
-/* One device-resident trajectory (the benchmark's unit of work): num_steps
+/* One device-resident trajectory (the benchmark's unit of work; replaces the
+ * time loop of inviscid_burgers_implicit2D, C/hypernet2D.py:72-131, with the
+ * snapshot matrix kept in HBM instead of host memory, :89-90,126): num_steps
  * march steps in ONE launch from the last uploaded state (from_initial = 1,
  * kept on the device by burg_upload_state) or from the resident state (0),
- * every intermediate state kept in HBM (the snapshot matrix, in the engine's
- * ring layout), the final state left resident.  Stream/pipe engines;
- * stats->loop_ms is the launch's device time (HIP events on the context's
- * stream). */
+ * the final state left resident.  The states kept in HBM (the snapshot
+ * matrix, in the engine's ring layout; see burg_trajectory_retained):
+ *   snap_every = 1: every state while the whole trajectory fits in 85 % of
+ *     free HBM; a larger one (8192 x 2048 and up x 500 steps) gets a ring
+ *     capped by free HBM that wraps inside the launch and keeps the last
+ *     states only;
+ *   snap_every = k >= 2: states 0, k, 2k, ..., floor(num_steps / k) k, in
+ *     retained windows of the ring at no extra HBM traffic (pipe engine;
+ *     narrow tiles with k < 1 + 64 / W keep every state, which must fit);
+ *   snap_every <= 0: 1 when the whole trajectory fits, else 10.
+ * Stream/pipe engines; stats->loop_ms is the launch's device time (HIP events
+ * on the context's stream).  burg_trajectory(ctx, T, f, st) is
+ * burg_trajectory_ex(ctx, T, 1, f, st). */
+int burg_trajectory_ex(burg_ctx *ctx, int num_steps, int snap_every, int from_initial,
+                       burg_stats *stats);
 int burg_trajectory(burg_ctx *ctx, int num_steps, int from_initial, burg_stats *stats);
-/* Allocate (or keep) everything burg_trajectory(ctx, num_steps, ...) needs --
- * the tiling, the edge mailboxes and the HBM ring of the trajectory (up to
- * 85 % of free HBM; 134 GB for 500 steps of 4096^2) -- without launching.
- * Multi-GPU slab ranks call it before the barrier that precedes their first
- * launch, so no rank's first launch waits for a neighbour's allocation. */
+/* Allocate (or keep) everything burg_trajectory_ex(ctx, num_steps,
+ * snap_every, ...) needs -- the tiling, the edge mailboxes and the HBM ring of
+ * the trajectory (up to 85 % of free HBM; 134 GB for 500 steps of 4096^2) --
+ * without launching.  Multi-GPU slab ranks call it before the barrier that
+ * precedes their first launch, so no rank's first launch waits for a
+ * neighbour's allocation. */
+int burg_reserve_trajectory_ex(burg_ctx *ctx, int num_steps, int snap_every);
 int burg_reserve_trajectory(burg_ctx *ctx, int num_steps);
+/* What burg_trajectory_ex(ctx, num_steps, snap_every) would keep, without
+ * allocating: the resolved snap_every (auto -> 1 or 10), the number of
+ * retained states (-1: a capped ring, known after the run) and the ring's
+ * bytes (0 when capped). */
+int burg_trajectory_plan(burg_ctx *ctx, int num_steps, int snap_every, int *snap_every_out,
+                         int64_t *retained_states, int64_t *ring_bytes);
+/* The states the last burg_trajectory_ex keeps resident: first_state,
+ * first_state + stride, ... (count of them; state q = after q steps).
+ * BURG_ESTATE when another run has since reused the ring. */
+int burg_trajectory_retained(burg_ctx *ctx, int64_t *first_state, int64_t *count, int *stride);
+/* Copy retained columns col0 .. col0 + ncols - 1 (column j = state
+ * first_state + j * stride) into the C-order (2n x ld_out) matrix `out`, at
+ * its columns 0 .. ncols - 1 -- the reference's snapshot layout
+ * (C/hypernet2D.py:89-90,126).  out_on_device = 0: host memory;
+ * 1: device memory of the context's GPU (e.g. for burg_pod_rsvd_device). */
+int burg_trajectory_copy(burg_ctx *ctx, int64_t col0, int64_t ncols, double *out, int64_t ld_out,
+                         int out_on_device);
 
 /* Parameter sweep (the reference's snapshot generation over a set of mu,
  * e.g. C/run_prom.py:59-71 over get_snapshot_params, C/run_tests.py:38-49):

@@ -39,12 +39,14 @@ def main():
     w0 = slab_state(np.ones(2 * N * ny), N, ny, rank, world)
     dist.barrier()
     mode = sys.argv[4] if len(sys.argv) > 4 else "run"
-    if mode == "failstate":
+    if mode in ("failstate", "failone"):
         # BURG_TEST_FAIL_DEVICE_HALO=1: the first launch fails as a stalled
-        # device halo ring would; the context must then refuse to launch
+        # device halo ring would; the context must then refuse to launch.
+        # failone (BURG_TEST_FAIL_DEVICE_HALO=R:1): only rank R's second
+        # launch fails; its neighbours' waits must give up by themselves
         from finitedifference_amd._lib import BurgersError
         codes = []
-        for _ in range(2):
+        for _ in range(2 if mode == "failstate" else 3):
             try:
                 ctx.run(w0, T)
                 codes.append(0)

@@ -396,8 +396,8 @@ def _run_slabs(tmp_path, N, T, world, mode="run", timeout=110, **env_extra):
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20",
-                   **{k: str(v) for k, v in env_extra.items()})
+                   MASTER_PORT=str(port), BURG_SPIN_SECONDS="20")
+        env.update({k: str(v) for k, v in env_extra.items()})
         procs.append(subprocess.Popen([sys.executable, worker, str(N), str(T), str(tmp_path),
                                        mode], env=env))
     codes = []

@@ -79,6 +79,28 @@ def test_ieee_slow_path_planted_bitwise(gpu, orc, nx, ny, engine, W, T):
     assert np.any((snaps[:, T] != 0) & (np.abs(snaps[:, T]) < 2.0 ** -1022))
 
 
+@pytest.mark.parametrize("nx,ny,engine,W", [(64, 64, "pipe", 16), (256, 64, "pipe", 64),
+                                           (128, 70, "stream", 0)])
+def test_large_h_fast_window_bitwise(gpu, orc, nx, ny, engine, W):
+    """The top of the fast window: with h_x = dt/4 / dx = 2^57
+    (dt = 2^60, allowed by burg_set_problem's (0, 2^100) bound) and mu2 = 5.56
+    the source term dt*0.02*exp(mu2*x) reaches 2^850 in the last columns, so
+    Cu is far above 2^798 and q = 0.25 + h_x Cu + h_y Cv above 2^900 --
+    outside the range sqrt_normal is verified on.  Those cells must take the
+    IEEE path (ieee_diagonals > 0) and the step must equal the oracle's IEEE
+    arithmetic bit for bit.  (Step 2 of this problem overflows: one step.)"""
+    dt, mu = 2.0 ** 60, (5.19, 5.56)
+    P = _problem(orc, nx, ny, dt=dt, mu=mu)
+    ref, _, _ = P.fom(np.ones(P.m), 1)
+    assert np.isfinite(ref[1]).all() and np.abs(ref[1]).max() > 2.0 ** 300
+    ctx = _ctx(nx, ny, dt=dt, mu=mu, engine=engine, stream_w=W)
+    snaps, st, _, _ = ctx.run(np.ones(P.m), 1)
+    if engine == "pipe":
+        assert st["engine"] == 2 and st["stream_w"] == W
+    assert st["ieee_diagonals"] > 0 and st["nonfinite_diagonals"] == 0
+    assert np.array_equal(snaps[:, 1], ref[1])
+
+
 def test_ieee_slow_path_planted_sweep_bitwise(gpu, orc):
     """The narrow sweep kernel (pipe_kernel<16, true>, the 1024^2 sweep's)
     with the planted w0: each trajectory bit-equal to the oracle for its mu."""
@@ -294,3 +316,63 @@ def test_failed_slab_context_refuses_launches(gpu, tmp_path):
     for r in range(2):
         codes = [int(x) for x in open(os.path.join(tmp_path, f"slab{r}.codes")).read().split()]
         assert codes == [BURG_EHIP, BURG_ESTATE], (r, codes)
+
+
+# The per-GPU shapes of the N > 1 bench lines (bench.py DEFAULT_SHAPES, DESIGN.md
+# section 8) and the whole 8192^2 grid on one GPU, at full size and full length:
+# the code path every rank of the driver's multi-GPU runs executes (rank 0's
+# slab is exactly this single-context grid; the other ranks differ only in
+# taking their south inflow from the halo ring).  dt = 0.05 * 1024 / nx, as the
+# bench.  Each trajectory ring is capped by free HBM (268 / 537 GB would be
+# needed) and wraps INSIDE the one launch.
+@pytest.mark.parametrize("nx,ny,W", [(8192, 2048, 256), (16384, 2048, 512), (8192, 8192, 1024)])
+def test_multi_gpu_rank_shape_500_steps_bitwise(gpu, orc, nx, ny, W):
+    """VERDICT r03 item 1 (C/hypernet2D.py:112-129): 500 steps from w0 = 1 in
+    ONE burg_trajectory launch at the planner's width; the final state equals
+    the oracle's row-pipelined march bit for bit, the last step is checked on
+    its own (orc_march_step(w_499) == w_500), and the IEEE-path count is
+    recorded (the inlet column's v leaves the fast window in the last ~20
+    steps at this CFL, as at 4096^2)."""
+    import time
+    T, dt = 500, 0.05 * 1024 / nx
+    P = _problem(orc, nx, ny, dt=dt)
+    t0 = time.perf_counter()
+    ref = P.march_traj(np.ones(P.m), T, snap_every=T)
+    t_orc = time.perf_counter() - t0
+    ctx = _ctx(nx, ny, dt=dt)
+    ctx.upload(np.ones(P.m))
+    st = ctx.trajectory(T)
+    print(f"\n{nx}x{ny}: W={st['stream_w']} tiles={st['stream_tiles']} "
+          f"launches={st['stream_launches']} ieee_diagonals={st['ieee_diagonals']} "
+          f"kernel {st['loop_ms']:.2f} ms ({nx * ny * T / st['loop_ms'] / 1e6:.1f} "
+          f"Gcell-updates/s), oracle {t_orc:.1f} s")
+    assert st["engine"] == 2 and st["stream_w"] == W
+    assert st["stream_launches"] == 1
+    assert st["nonfinite_diagonals"] == 0
+    assert st["ieee_diagonals"] > 0
+    w500 = ctx.download()
+    assert np.array_equal(w500, ref[-1])
+    st2 = ctx.trajectory(T - 1)
+    assert st2["stream_launches"] == 1
+    w499 = ctx.download()
+    assert np.array_equal(P.march_step(w499), w500)
+    ctx.close()
+
+
+def test_one_rank_fails_at_a_later_launch(gpu, tmp_path):
+    """ONE rank's launch k > 0 fails (test hook
+    BURG_TEST_FAIL_DEVICE_HALO=1:1, rank 1's second launch) while its
+    neighbour keeps launching: the neighbour's bounded waits give up by
+    themselves (BURG_EHIP; T = 12 steps > the 8 halo slots, so the producer
+    below must stall), and both contexts then refuse further launches
+    (BURG_ESTATE) -- every rank ends failed, which bench.py's agreement turns
+    into one collective fall-back (rehearsal: tools/gpu_r4.sh)."""
+    from test_gpu_parity import _run_slabs
+    from finitedifference_amd._lib import BURG_EHIP, BURG_ESTATE
+    import os
+    _run_slabs(tmp_path, 96, 12, 2, mode="failone", BURG_TEST_FAIL_DEVICE_HALO="1:1",
+               BURG_SPIN_SECONDS="3")
+    codes = [[int(x) for x in open(os.path.join(tmp_path, f"slab{r}.codes")).read().split()]
+             for r in range(2)]
+    assert codes[1] == [0, BURG_EHIP, BURG_ESTATE], codes
+    assert codes[0] == [0, BURG_EHIP, BURG_ESTATE], codes

@@ -1,5 +1,6 @@
 // LDS-DMA above 64 KB: one wave DMAs 1 KB rows (buffer_load_dwordx4 ... lds)
-// into a dynamic LDS image at offsets 0 .. 150 KB and checks every word --
+// into a dynamic LDS image at offsets 0 .. 160 KB (the whole CU) and checks
+// every word --
 // does the pipe engine's wide-tile window have to sit below 64 KB?
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -28,7 +29,7 @@ __global__ void probe(const v4u *src, unsigned *bad, int rows)
 }
 int main()
 {
-    const int rows = 150;  // 150 KB
+    const int rows = 160;  // 160 KB: the whole LDS of a CU
     std::vector<unsigned> h(rows * 256);
     for (size_t i = 0; i < h.size(); ++i) h[i] = 0x1000u + (unsigned)i;
     v4u *d; unsigned *b;
