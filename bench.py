@@ -324,15 +324,29 @@ def rom_pipeline(N=250, T=500, npod=95, rom_steps=20):
     (DESIGN.md section 4.6)."""
     from finitedifference_amd import hypernet2D as H
     from finitedifference_amd.solver import FOMContext
+    import torch
     gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
     m = 2 * N * N
+    H.inviscid_burgers_implicit2D_sweep(gx, gy, np.ones(m), DT, 2, ROM_MUS, verbose=0)  # warm
     t0 = time.perf_counter()
-    sn = H.inviscid_burgers_implicit2D_sweep(gx, gy, np.ones(m), DT, T, ROM_MUS, verbose=0)
+    sn, sst = H.inviscid_burgers_implicit2D_sweep(gx, gy, np.ones(m), DT, T, ROM_MUS, verbose=0,
+                                                  return_stats=True)
     t_sweep = time.perf_counter() - t0
     S = np.hstack(sn)
     del sn
     u, s, pod_ms = H.POD(S, num_modes=npod, method="rsvd", random_state=0, return_ms=True)
     del S
+    # the same flow with the snapshot set left on the device (burg_sweep_device
+    # -> burg_pod_rsvd_device): no 4.5 GB host round trip
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    Sd, dst = H.inviscid_burgers_implicit2D_sweep(gx, gy, np.ones(m), DT, T, ROM_MUS, verbose=0,
+                                                  on_device=True, return_stats=True)
+    ud, sd, pod_ms_dev = H.POD(Sd, num_modes=npod, method="rsvd", random_state=0, return_ms=True)
+    t_dev = time.perf_counter() - t0
+    del Sd
+    torch.cuda.empty_cache()
+    pod_match = float(np.max(np.abs(sd - s) / s[0]))
     ctx = FOMContext(N, N)
     ctx.set_problem(gx, gy, DT, (4.75, 0.02))
     ctx.lspg(np.ones(m), 1, u, keep_snaps=False)  # warm-up
@@ -343,6 +357,16 @@ def rom_pipeline(N=250, T=500, npod=95, rom_steps=20):
     alg = 2 * m * npod * 8 + 4 * m * 8
     return {"grid": f"{N}x{N}", "training": f"{len(ROM_MUS)} mu x {T} steps", "npod": npod,
             "fom_sweep_s_incl_d2h": round(t_sweep, 3), "pod_rsvd_device_ms": round(pod_ms, 2),
+            "fom_sweep_kernel_ms": round(sst["loop_ms"], 3),
+            "fom_sweep_launches": sst["stream_launches"],
+            "fom_sweep_tile_w": sst["stream_w"],
+            "fom_sweep_gcell_per_s": round(m // 2 * T * len(ROM_MUS) / sst["loop_ms"] / 1e6, 2),
+            "sweep_to_pod_on_device_s": round(t_dev, 3),
+            "sweep_to_pod_on_device_detail": {
+                "sweep_kernel_ms": round(dst["loop_ms"], 3), "pod_ms": round(pod_ms_dev, 2),
+                "what": "burg_sweep_device (the 9 trajectories side by side, snapshot set left "
+                        "in HBM) + burg_pod_rsvd_device, wall clock",
+                "sigma_max_rel_diff_vs_host_path": pod_match},
             "lspg_ms_per_step": round(st["loop_ms"] / rom_steps, 4),
             "lspg_gn_norms_per_step": float(its.mean()),
             "lspg_gram": {"avg_launch_ms": round(gram_ms, 4), "alg_bytes": alg,

@@ -28,6 +28,7 @@ EXPORTS = (
     "burg_advance", "burg_download_state", "burg_set_engine", "burg_trajectory",
     "burg_reserve_trajectory", "burg_trajectory_ex", "burg_reserve_trajectory_ex",
     "burg_trajectory_plan", "burg_trajectory_retained", "burg_trajectory_copy",
+    "burg_sweep_device", "burg_pod_rsvd_device",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
     "burg_pod", "burg_pod_rsvd", "burg_run_npy",
 )
@@ -170,6 +171,12 @@ def load(path=None):
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),
+            "burg_sweep_device": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                                                 ctypes.POINTER(BurgStats)]),
+            "burg_pod_rsvd_device": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+                                                    ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                                    ctypes.c_int, _D, _D, _D, _D]),
         }
         for name, (res, args) in sig.items():
             fn = getattr(lib, name)

@@ -186,6 +186,8 @@ struct burg_ctx {
     // tables bat_colc_stride apart (ov_colc)
     int bat_nd = 1, bat_ny_d = 0;
     size_t bat_colc_stride = 0;
+    burg_ctx *bat_child = nullptr;  // the parent's cached side-by-side sweep context
+    int bat_child_G = 0;
     double *d_halo_rows = nullptr;   // burg_slab_residual: the south halo rows of w, wp (4 nx)
     TrajRecord tr;                   // the last trajectory's resident states
     double *d_ret0 = nullptr;        // its initial state (retained windows: the working ring
@@ -1504,6 +1506,7 @@ void burg_ctx_destroy(burg_ctx *c)
     dfree(c->d_sumsq);
     dfree(c->d_halo_rows);
     dfree(c->d_ret0);
+    if (c->bat_child) burg_ctx_destroy(c->bat_child);
     stream_free(c);
     if (c->halo_out_ipc) (void)hipIpcCloseMemHandle(c->halo_out_ipc);
     if (c->halo_in_ring) (void)hipFree(c->halo_in_ring);
@@ -1927,10 +1930,251 @@ int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, 
     return rc;
 }
 
-int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,
-               double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *st)
+static int check_device_ptr(const burg_ctx *c, const void *p, const char *what);
+
+// Where a sweep's snapshot matrices go: nmu host matrices (C-order, leading
+// dimension ld_host) or one device matrix (C-order, ld_dev) holding mu j's
+// columns at j * ncols ... (j + 1) * ncols - 1 (np.hstack of the per-mu
+// matrices, as C/run_prom.py:59-71 builds it); neither: states stay in HBM.
+struct SweepOut {
+    double *const *host = nullptr;
+    int64_t ld_host = 0;
+    double *dev = nullptr;
+    int64_t ld_dev = 0;
+};
+
+// Side-by-side sweep groups: how many trajectories of this grid run at once
+// as separate domains of one launch (0: none -- the grid alone fills half the
+// chip or more, a slab, or a forced tile width).  BURG_SWEEP_BATCH=G forces G
+// (1: off).
+constexpr int kBatchMax = 16;
+int batch_group(burg_ctx *c, int nmu)
 {
-    BURG_TRACE("burg_sweep");
+    if (c->world > 1 || nmu < 2 || c->eng_eff != BURG_ENGINE_PIPE) return 0;
+    if (const char *e = std::getenv("BURG_SWEEP_BATCH")) {
+        const int v = std::atoi(e);
+        return v >= 2 ? std::min({v, nmu, kBatchMax}) : 0;
+    }
+    if (c->stream_w_opt != 0 || c->tiles_target_opt != 0) return 0;
+    const int wgs = c->sp.nti * c->nwj;
+    const int cap = pipe_max_resident_blocks(c->sp.W, false);
+    if (cap <= 0 || 2 * wgs > cap) return 0;
+    return std::min({nmu, cap / wgs, kBatchMax});
+}
+
+// burg_sweep for small grids: the reference's
+// drivers run a snapshot set one trajectory at a time (C/run_prom.py:59-71);
+// a 250^2 grid fills ~32 of 256 CUs, so G trajectories run side by side as G
+// independent domains stacked in ONE launch of an internal context (each
+// domain's rows padded to whole strips; its own column table (mu2) and inlet
+// rows (mu1)).  Every trajectory is the same exact march, bit for bit.
+// Returns 1 when the mode does not apply (the caller runs the serial sweep).
+static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b,
+                              int T, int snap_every, const SweepOut &out, burg_stats *st)
+{
+    const int G = batch_group(c, nmu);
+    if (G < 2) return 1;
+    const int nx = c->nx, ny = c->nrows;
+    const int nti_d = (ny + kWave - 1) / kWave, ny_pad = nti_d * kWave;
+    const size_t m = c->m(), n = c->n();
+    const int64_t ncols = T / snap_every + 1;
+    if (!c->bat_child || c->bat_child_G != G) {
+        if (c->bat_child) burg_ctx_destroy(c->bat_child);
+        c->bat_child = nullptr;
+        burg_ctx *ch = nullptr;
+        if (int e = burg_ctx_create(c->device, nx, G * ny_pad, &ch)) return e;
+        ch->bat_nd = G;
+        ch->bat_ny_d = ny;
+        c->bat_child = ch;
+        c->bat_child_G = G;
+    }
+    burg_ctx *ch = c->bat_child;
+    ch->spin_ticks = c->spin_ticks;
+    ch->engine = BURG_ENGINE_PIPE;
+    // host copies of the grid's coefficient rows and of w0
+    std::vector<double> ix(nx), iy(ny), w0(m);
+    HIPCHK(hipMemcpy(ix.data(), c->cf.inv_dx, sizeof(double) * nx, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(iy.data(), c->cf.inv_dy, sizeof(double) * ny, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(w0.data(), c->d_w0, sizeof(double) * m, hipMemcpyDeviceToHost));
+    const size_t nc = ch->n(), dpl = (size_t)ny_pad * nx;  // child plane, one domain's rows
+    std::vector<double> iyt((size_t)G * ny_pad), lbt((size_t)G * ny_pad), w0s(2 * nc, 1.0);
+    for (int j = 0; j < G; ++j)
+        for (int r = 0; r < ny_pad; ++r) iyt[(size_t)j * ny_pad + r] = iy[std::min(r, ny - 1)];
+    for (int j = 0; j < G; ++j) {
+        std::memcpy(&w0s[j * dpl], &w0[0], sizeof(double) * n);
+        std::memcpy(&w0s[nc + j * dpl], &w0[n], sizeof(double) * n);
+    }
+    double *d_srcb = nullptr, *d_tr = nullptr;
+    d2 *d_colcb = nullptr;
+    bool registered = false;
+    int S = 0;
+    auto cleanup = [&]() {
+        ch->ov_colc = nullptr;
+        (void)hipStreamSynchronize(ch->stream);
+        (void)hipStreamSynchronize(c->stream);
+        if (registered)
+            for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(out.host[j]);
+        dfree(d_srcb);
+        dfree(d_colcb);
+        dfree(d_tr);
+    };
+    int rc = BURG_OK;
+    double ms = 0.0, flush_ms = 0.0;
+    int64_t ieee = 0, launches = 0, polls = 0, slow = 0, spins = 0;
+    std::vector<double> srcg((size_t)G * nx);
+    for (int g0 = 0; g0 < nmu && rc == BURG_OK; g0 += G) {
+        const int nb = std::min(G, nmu - g0);
+        for (int j = 0; j < G; ++j) {
+            const int mj = g0 + std::min(j, nb - 1);  // (a short last group repeats its last mu)
+            for (int r = 0; r < ny_pad; ++r)
+                lbt[(size_t)j * ny_pad + r] =
+                    lbc_b[(size_t)mj * c->ny_total + c->row0 + std::min(r, ny - 1)];
+            std::memcpy(&srcg[(size_t)j * nx], src_b + (size_t)mj * nx, sizeof(double) * nx);
+        }
+        if ((rc = burg_set_problem(ch, ix.data(), iyt.data(), srcg.data(), lbt.data(), c->dt))) break;
+        if ((rc = stream_setup(ch))) break;
+        if (ch->eng_eff != BURG_ENGINE_PIPE) {
+            if (g0 == 0) {
+                cleanup();
+                return 1;  // the stacked grid does not fit resident: serial sweep
+            }
+            rc = fail(BURG_ESHAPE, "side-by-side sweep lost its pipe plan");
+            break;
+        }
+        const size_t ncolp = (size_t)ch->sp.ntj * ch->sp.W;
+        if (!d_srcb) {
+            if ((rc = dalloc(&d_srcb, (size_t)G * nx)) || (rc = dalloc(&d_colcb, (size_t)G * ncolp)))
+                break;
+            if (out.host) {
+                size_t freeb = 0, totalb = 0;
+                HIPCHK(hipMemGetInfo(&freeb, &totalb));
+                S = (int)std::min<int64_t>(ncols, 64);
+                while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
+                if ((rc = dalloc(&d_tr, (size_t)S * m))) break;
+                registered = true;
+                for (int j = 0; j < nmu; ++j)
+                    if (hipHostRegister(out.host[j], m * out.ld_host * sizeof(double),
+                                        hipHostRegisterDefault) != hipSuccess) {
+                        (void)hipGetLastError();
+                        for (int i = 0; i < j; ++i) (void)hipHostUnregister(out.host[i]);
+                        registered = false;
+                        break;
+                    }
+            }
+        }
+        HIPCHK(hipMemcpyAsync(d_srcb, srcg.data(), sizeof(double) * G * nx, hipMemcpyHostToDevice,
+                              ch->stream));
+        CHK(launch_colc_batch(ch->cf, G, d_srcb, (int)ncolp, d_colcb, ch->stream));
+        ch->bat_colc_stride = ncolp;
+        ch->ov_colc = d_colcb;
+        if ((rc = burg_upload_state(ch, w0s.data()))) break;
+        burg_stats cst{};
+        rc = stream_trajectory(ch, T, snap_every, true, &cst);
+        ch->ov_colc = nullptr;
+        if (rc) break;
+        const TrajRecord &tr = ch->tr;
+        if (!(tr.valid && tr.first == 0 && tr.stride == snap_every && tr.count == ncols)) {
+            rc = fail(BURG_ENOMEM, "side-by-side sweep: the %d-trajectory group's states do not "
+                      "fit in HBM", G);
+            break;
+        }
+        ms += cst.loop_ms;
+        ieee += cst.ieee_diagonals;
+        polls += cst.comm_polls;
+        slow += cst.slow_diagonals;
+        spins += cst.stall_spins;
+        ++launches;
+        // each domain's snapshot columns: 0 = w0, k = state k * snap_every
+        hipEvent_t f0 = nullptr, f1 = nullptr;
+        (void)hipEventCreate(&f0);
+        (void)hipEventCreate(&f1);
+        (void)hipEventRecord(f0, ch->stream);
+        const int W = ch->sp.W;
+        for (int j = 0; j < nb && rc == BURG_OK && (out.host || out.dev); ++j) {
+            StreamArgs va = stream_args(ch, tr.map.L, tr.map.origin, 0, &tr.map);
+            va.ring += (size_t)j * nti_d * ch->sp.ntj * (size_t)va.Lt * kWave;
+            va.cf.ny = ny;
+            va.nti = nti_d;
+            va.ntiles = nti_d * ch->sp.ntj;
+            if (out.dev) {
+                double *dst = out.dev + (size_t)(g0 + j) * ncols;
+                const int ldo = (int)out.ld_dev;
+                const double *p0 = c->d_w0;
+                if (launch_transpose(&p0, 1, m, dst, ldo, ch->stream) ||
+                    (ncols > 1 && launch_ring_extract(va, W, snap_every, snap_every, (int)(ncols - 1),
+                                                      dst + 1, ldo, ch->stream)))
+                    rc = fail(BURG_EHIP, "sweep snapshot extract failed");
+                continue;
+            }
+            double *dst = out.host[g0 + j];
+            const double *p0 = c->d_w0;
+            for (int64_t k0 = 0; k0 < ncols && rc == BURG_OK; k0 += S) {
+                const int cnt = (int)std::min<int64_t>(S, ncols - k0);
+                int e = 0;
+                if (k0 == 0) {
+                    e = launch_transpose(&p0, 1, m, d_tr, S, ch->stream);
+                    if (!e && cnt > 1)
+                        e = launch_ring_extract(va, W, snap_every, snap_every, cnt - 1, d_tr + 1, S,
+                                                ch->stream);
+                } else {
+                    e = launch_ring_extract(va, W, (int)(k0 * snap_every), snap_every, cnt, d_tr, S,
+                                            ch->stream);
+                }
+                if (e || hipMemcpy2DAsync(dst + k0, (size_t)out.ld_host * sizeof(double), d_tr,
+                                          (size_t)S * sizeof(double), (size_t)cnt * sizeof(double),
+                                          m, hipMemcpyDeviceToHost, ch->stream) != hipSuccess ||
+                    hipStreamSynchronize(ch->stream) != hipSuccess)
+                    rc = fail(BURG_EHIP, "sweep snapshot copy failed");
+            }
+        }
+        (void)hipEventRecord(f1, ch->stream);
+        (void)hipEventSynchronize(f1);
+        float t = 0.f;
+        (void)hipEventElapsedTime(&t, f0, f1);
+        flush_ms += t;
+        (void)hipEventDestroy(f0);
+        (void)hipEventDestroy(f1);
+        if (rc == BURG_OK && g0 + nb == nmu) {
+            // the last trajectory's final state becomes the parent's resident state
+            const double *fs = ch->d_state[ch->cur] + (size_t)(nb - 1) * dpl;
+            double *dstate = c->d_state[c->cur ^ 1];
+            if (hipMemcpyAsync(dstate, fs, sizeof(double) * n, hipMemcpyDeviceToDevice, ch->stream) !=
+                    hipSuccess ||
+                hipMemcpyAsync(dstate + n, fs + nc, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                               ch->stream) != hipSuccess ||
+                hipStreamSynchronize(ch->stream) != hipSuccess)
+                rc = fail(BURG_EHIP, "resident state copy failed");
+            else
+                c->cur ^= 1;
+        }
+    }
+    if (st) {
+        st->steps = (int64_t)nmu * T;
+        st->passes = st->steps;
+        st->max_passes = 1;
+        st->engine = BURG_ENGINE_PIPE;
+        st->stream_w = ch->sp.W;
+        st->stream_tiles = ch->sp.ntiles;
+        st->loop_ms = ms;
+        st->march_kernel_ms = ms;
+        st->flush_ms = flush_ms;
+        st->march_launches = launches;
+        st->stream_launches = launches;
+        st->ieee_diagonals = ieee;
+        st->comm_polls = polls;
+        st->slow_diagonals = slow;
+        st->stall_spins = spins;
+        st->tile_marches = (int64_t)nmu * T * (c->sp.ntiles > 0 ? c->sp.ntiles : 1);
+    }
+    cleanup();
+    return rc;
+}
+
+static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b,
+                      int num_steps, const SweepOut &out, int snap_every, burg_stats *st)
+{
+    double *const *snaps = out.host;
+    const int64_t ld_snaps = out.ld_host;
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (nmu < 1) return fail(BURG_EINVAL, "nmu must be >= 1");
@@ -1945,12 +2189,22 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
         for (int j = 0; j < nmu; ++j)
             if (!snaps[j]) return fail(BURG_EINVAL, "null snapshot matrix %d", j);
     }
+    if (out.dev) {
+        if (out.ld_dev < (int64_t)nmu * ncols || out.ld_dev > INT32_MAX)
+            return fail(BURG_EINVAL, "ld_out=%lld: need nmu * (num_steps / snap_every + 1) = %lld "
+                        "columns", (long long)out.ld_dev, (long long)nmu * ncols);
+        if (int e = check_device_ptr(c, out.dev, "out")) return e;
+    }
     if (c->engine == BURG_ENGINE_TILES) return fail(BURG_EINVAL, "burg_sweep runs on the pipe engine");
     if (!c->d_w0) return fail(BURG_ESTATE, "burg_sweep: upload the initial state first");
     if (int e = stream_setup(c)) return e;
     if (c->eng_eff != BURG_ENGINE_PIPE)
         return fail(BURG_ESHAPE, "burg_sweep runs on the pipe engine; this %d x %d grid needs "
                     "the streaming engine's wider tiles", c->nx, c->nrows);
+    {
+        const int r = sweep_side_by_side(c, nmu, src_b, lbc_b, num_steps, snap_every, out, st);
+        if (r <= 0) return r;  // done (or failed); 1: the serial sweep below
+    }
     // narrow tiles run a group of trajectories per launch (the sweep kernel);
     // wide tiles one launch per trajectory with that mu's coefficient tables
     const bool narrow = pipe_sweep_width_supported(c->sp.W);
@@ -2060,6 +2314,20 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
         if (rc) break;
         ++launches;
         last_nb = nb;
+        if (out.dev) {
+            // straight into the device matrix: column 0 = w0, then the states
+            for (int j = 0; j < nb && rc == BURG_OK; ++j) {
+                double *dst = out.dev + (size_t)(g0 + j) * ncols;
+                const double *p0 = c->d_w0;
+                if (launch_transpose(&p0, 1, m, dst, (int)out.ld_dev, c->stream) ||
+                    (ncols > 1 && launch_ring_extract(stream_args(c, L, 0, 0), W,
+                                                      (int)(j * T + snap_every), snap_every,
+                                                      (int)(ncols - 1), dst + 1, (int)out.ld_dev,
+                                                      c->stream)))
+                    rc = fail(BURG_EHIP, "snapshot extract failed");
+            }
+            continue;
+        }
         if (!snaps) continue;
         (void)hipEventRecord(f0, c->stream);
         for (int j = 0; j < nb && rc == BURG_OK; ++j) {
@@ -2108,6 +2376,28 @@ int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, i
     (void)hipEventDestroy(f1);
     cleanup();
     return rc;
+}
+
+int burg_sweep(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b, int num_steps,
+               double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *st)
+{
+    BURG_TRACE("burg_sweep");
+    SweepOut so;
+    so.host = snaps;
+    so.ld_host = ld_snaps;
+    return sweep_impl(c, nmu, src_b, lbc_b, num_steps, so, snap_every, st);
+}
+
+int burg_sweep_device(burg_ctx *c, int nmu, const double *src_b, const double *lbc_b,
+                      int num_steps, int snap_every, double *d_out, int64_t ld_out,
+                      burg_stats *st)
+{
+    BURG_TRACE("burg_sweep_device");
+    if (!d_out) return fail(BURG_EINVAL, "null output");
+    SweepOut so;
+    so.dev = d_out;
+    so.ld_dev = ld_out;
+    return sweep_impl(c, nmu, src_b, lbc_b, num_steps, so, snap_every, st);
 }
 
 int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const double *prev_states,
@@ -2828,10 +3118,35 @@ int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *
     return burg_pod_rsvd(device, m, ns, snaps, k, 0, 0, nullptr, U, sigma, ms);
 }
 
+static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool snaps_on_device, int k,
+                    int nrand, int n_iter, const double *omega, double *U, double *sigma, double *ms);
+
 int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
                   const double *omega, double *U, double *sigma, double *ms)
 {
     BURG_TRACE("burg_pod_rsvd");
+    return pod_impl(device, m, ns, snaps, false, k, nrand, n_iter, omega, U, sigma, ms);
+}
+
+int burg_pod_rsvd_device(int device, int64_t m, int ns, const double *d_snaps, int k, int nrand,
+                         int n_iter, const double *omega, double *U, double *sigma, double *ms)
+{
+    BURG_TRACE("burg_pod_rsvd_device");
+    if (d_snaps) {
+        hipPointerAttribute_t at{};
+        if (hipPointerGetAttributes(&at, d_snaps) != hipSuccess || at.type != hipMemoryTypeDevice ||
+            at.device != device) {
+            (void)hipGetLastError();
+            return fail(BURG_EINVAL, "burg_pod_rsvd_device: snaps is not device memory of GPU %d",
+                        device);
+        }
+    }
+    return pod_impl(device, m, ns, d_snaps, true, k, nrand, n_iter, omega, U, sigma, ms);
+}
+
+static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool snaps_on_device, int k,
+                    int nrand, int n_iter, const double *omega, double *U, double *sigma, double *ms)
+{
     if (!snaps || !U || !sigma) return fail(BURG_EINVAL, "null array");
     if (omega && (nrand < k || nrand > ns || n_iter < 0))
         return fail(BURG_EINVAL, "burg_pod_rsvd: need k <= nrand <= ns and n_iter >= 0");
@@ -2852,16 +3167,19 @@ int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int
     };
     const size_t mm = (size_t)m;
     int rc = BURG_OK;
-    if ((rc = dalloc(&d_s, mm * ns)) || (rc = dalloc(&d_u, mm * k)) || (rc = dalloc(&d_sig, (size_t)k))) {
+    if ((!snaps_on_device && (rc = dalloc(&d_s, mm * ns))) || (rc = dalloc(&d_u, mm * k)) ||
+        (rc = dalloc(&d_sig, (size_t)k))) {
         cleanup();
         return rc;
     }
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
-    if (hipMemcpyAsync(d_s, snaps, sizeof(double) * mm * ns, hipMemcpyHostToDevice, st) != hipSuccess) {
+    if (!snaps_on_device &&
+        hipMemcpyAsync(d_s, snaps, sizeof(double) * mm * ns, hipMemcpyHostToDevice, st) != hipSuccess) {
         cleanup();
         return fail(BURG_EHIP, "burg_pod: snapshot upload failed");
     }
+    const double *d_in = snaps_on_device ? snaps : d_s;
     if (omega) {
         if ((rc = dalloc(&d_om, (size_t)ns * nrand))) {
             cleanup();
@@ -2875,9 +3193,9 @@ int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int
     }
     (void)hipEventRecord(e0, st);
     char msg[256] = {0};
-    const int r = omega ? pod_rsvd_device(st, mm, ns, d_s, k, nrand, n_iter, d_om, d_u, d_sig, msg,
+    const int r = omega ? pod_rsvd_device(st, mm, ns, d_in, k, nrand, n_iter, d_om, d_u, d_sig, msg,
                                           sizeof msg)
-                        : pod_device(st, mm, ns, d_s, k, d_u, d_sig, msg, sizeof msg);
+                        : pod_device(st, mm, ns, d_in, k, d_u, d_sig, msg, sizeof msg);
     (void)hipEventRecord(e1, st);
     if (r != 0) {
         cleanup();

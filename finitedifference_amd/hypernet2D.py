@@ -127,19 +127,28 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
 
 def inviscid_burgers_implicit2D_sweep(grid_x, grid_y, w0, dt, num_steps, mus, *, snap_every=1,
                                       device=0, verbose=1, allow_nonsquare=False,
-                                      return_stats=False, outs=None):
+                                      return_stats=False, outs=None, on_device=False):
     """inviscid_burgers_implicit2D (C/hypernet2D.py:72-131) for a LIST of mu at
     once -- what the reference's drivers do one call at a time when they fill
     a snapshot set (C/run_prom.py:59-71 over the 9 get_snapshot_params,
-    C/run_tests.py:38-49 over 3 test mu).  All trajectories start from w0,
-    run back to back in one pipelined launch on the GPU (burg_sweep) and are
-    each bit-identical to inviscid_burgers_implicit2D(..., mu) with the march
-    solver.  Returns a list of snapshot matrices, one per mu."""
+    C/run_tests.py:38-49 over 3 test mu).  All trajectories start from w0 and
+    run in one pipelined launch per group on the GPU (burg_sweep): back to
+    back in time, or -- grids that leave most of the chip idle, such as the
+    reference's own 250^2 -- side by side as separate domains; each is
+    bit-identical to inviscid_burgers_implicit2D(..., mu) with the march
+    solver.  Returns a list of snapshot matrices, one per mu; on_device=True
+    returns ONE float64 CUDA tensor, the np.hstack of those matrices
+    (C/run_prom.py:59-71's snapshot set) left in HBM (burg_sweep_device), which
+    POD(...) factorises in place."""
     mus = [tuple(mu) for mu in mus]
     if verbose:
         for mu in mus:
             print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mus[0], device, allow_nonsquare, engine="pipe")
+    if on_device:
+        S, stats = ctx.sweep_device(mus, int(num_steps), w0=np.asarray(w0, dtype=np.float64).ravel(),
+                                    snap_every=int(snap_every))
+        return (S, stats) if return_stats else S
     snaps, stats = ctx.sweep(mus, int(num_steps), w0=np.asarray(w0, dtype=np.float64).ravel(),
                              snap_every=int(snap_every), outs=outs)
     if return_stats:
@@ -293,9 +302,21 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
     if method not in ("svd", "rsvd"):
         raise ValueError("Unknown method '{}' for POD. Use 'svd' or 'rsvd'.".format(method))
     from . import _lib
-    S = np.ascontiguousarray(np.asarray(snaps, dtype=np.float64))
-    if S.ndim != 2:
-        raise ValueError("snaps must be a 2-D (dofs, snapshots) matrix")
+    on_dev = type(snaps).__module__.startswith("torch")
+    if on_dev:
+        # a device-resident snapshot matrix (e.g. inviscid_burgers_implicit2D_sweep(...,
+        # on_device=True)): factorised in place, no host round trip
+        import torch
+        if (snaps.dtype != torch.float64 or snaps.dim() != 2 or not snaps.is_contiguous()
+                or snaps.device.type != "cuda"):
+            raise ValueError("a device snapshot matrix must be a contiguous 2-D float64 CUDA tensor")
+        device = snaps.device.index if snaps.device.index is not None else 0
+        torch.cuda.synchronize(snaps.device)
+        S = snaps
+    else:
+        S = np.ascontiguousarray(np.asarray(snaps, dtype=np.float64))
+        if S.ndim != 2:
+            raise ValueError("snaps must be a 2-D (dofs, snapshots) matrix")
     m, ns = S.shape
     if m < ns:
         raise ValueError("POD on the GPU needs at least as many rows as snapshots")
@@ -305,8 +326,12 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
     ms = ctypes.c_double(0.0)
     L = _lib.load()
     if method == "svd":
-        _lib.check(L.burg_pod(int(device), m, ns, _lib.dptr(S), k, _lib.dptr(u), _lib.dptr(sv),
-                              ctypes.byref(ms)))
+        if on_dev:
+            _lib.check(L.burg_pod_rsvd_device(int(device), m, ns, S.data_ptr(), k, 0, 0, None,
+                                              _lib.dptr(u), _lib.dptr(sv), ctypes.byref(ms)))
+        else:
+            _lib.check(L.burg_pod(int(device), m, ns, _lib.dptr(S), k, _lib.dptr(u), _lib.dptr(sv),
+                                  ctypes.byref(ms)))
     else:
         if random_state is None:
             rng = np.random.mtrand._rand
@@ -322,9 +347,14 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
         omega = rng.normal(size=(ns, k + 10))
         nrand = min(k + 10, ns)
         omega_cm = np.ascontiguousarray(omega[:, :nrand].T)  # column-major (ns x nrand)
-        _lib.check(L.burg_pod_rsvd(int(device), m, ns, _lib.dptr(S), k, nrand, n_iter,
-                                   _lib.dptr(omega_cm), _lib.dptr(u), _lib.dptr(sv),
-                                   ctypes.byref(ms)))
+        if on_dev:
+            _lib.check(L.burg_pod_rsvd_device(int(device), m, ns, S.data_ptr(), k, nrand, n_iter,
+                                              _lib.dptr(omega_cm), _lib.dptr(u), _lib.dptr(sv),
+                                              ctypes.byref(ms)))
+        else:
+            _lib.check(L.burg_pod_rsvd(int(device), m, ns, _lib.dptr(S), k, nrand, n_iter,
+                                       _lib.dptr(omega_cm), _lib.dptr(u), _lib.dptr(sv),
+                                       ctypes.byref(ms)))
     return (u, sv, ms.value) if return_ms else (u, sv)
 
 

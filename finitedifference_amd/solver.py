@@ -297,6 +297,44 @@ class FOMContext:
                                       ctypes.byref(st)))
         return snaps, st.as_dict()
 
+    def _sweep_tables(self, mus):
+        gx, gy, dt, nonsq = self._grid
+        src_b, lbc_b = [], []
+        for mu in mus:
+            _, _, src, lbc = fom_coefficients(gx, gy, dt, mu, nonsq)
+            src_b.append(src)
+            lbc_b.append(lbc)
+        return np.ascontiguousarray(np.stack(src_b)), np.ascontiguousarray(np.stack(lbc_b))
+
+    def sweep_device(self, mus, num_steps, w0=None, snap_every=1, out=None):
+        """sweep() with the snapshot set left in HBM (burg_sweep_device):
+        returns (a float64 CUDA tensor (m, len(mus) * ncols) = np.hstack of the
+        per-mu snapshot matrices -- `out` if given, written in place --,
+        stats)."""
+        import torch
+        if getattr(self, "_grid", None) is None:
+            raise RuntimeError("set_problem first")
+        mus = [tuple(float(x) for x in mu) for mu in mus]
+        if not mus:
+            raise ValueError("empty mu list")
+        src_b, lbc_b = self._sweep_tables(mus)
+        if w0 is not None:
+            self.upload(w0)
+        ncols = num_steps // snap_every + 1
+        dev = torch.device("cuda", self.device)
+        if out is None:
+            out = torch.empty((self.m, len(mus) * ncols), dtype=torch.float64, device=dev)
+        elif (out.dtype != torch.float64 or out.device != dev or not out.is_contiguous()
+              or out.dim() != 2 or out.shape[0] != self.m or out.shape[1] < len(mus) * ncols):
+            raise ValueError(f"out must be a contiguous float64 ({self.m}, >= {len(mus) * ncols}) "
+                             f"tensor on {dev}")
+        torch.cuda.current_stream(dev).synchronize()
+        st = _lib.BurgStats()
+        _lib.check(self._L.burg_sweep_device(self._h, len(mus), _lib.dptr(src_b), _lib.dptr(lbc_b),
+                                             int(num_steps), int(snap_every), out.data_ptr(),
+                                             int(out.shape[1]), ctypes.byref(st)))
+        return out, st.as_dict()
+
     def ecsw_matrix(self, snaps, prev_snaps, basis, return_stats=False):
         """ECSW training matrix (burg_ecsw_matrix) of snapshot columns
         snaps[:, i] with previous states prev_snaps[:, i] and a (2n, npod)

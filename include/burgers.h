@@ -28,6 +28,9 @@
  *                       with C/hypernet2D.py:1859-1929 gauss_newton_LSPG
  *   burg_pod            C/hypernet2D.py:2670-2695   POD(method='svd') (np.linalg.svd)
  *   burg_pod_rsvd       C/hypernet2D.py:2688-2692   POD(method='rsvd') (randomized_svd)
+ *   burg_pod_rsvd_device  the same on a device-resident snapshot matrix
+ *   burg_sweep_device   C/run_prom.py:59-71  the training snapshot set, left on the device
+ *   burg_trajectory_ex  C/hypernet2D.py:72-131  the time loop, snapshots kept in HBM
  *   burg_set_problem    C/hypernet2D.py:2410-2416, 2425-2431, 2536-2554
  *                       (make_ddx / make_2D_grid spacings, source, inlet BC)
  *
@@ -298,6 +301,16 @@ int burg_trajectory_copy(burg_ctx *ctx, int64_t col0, int64_t ncols, double *out
  * trajectory's final state becomes the resident state.  Pipe engine only. */
 int burg_sweep(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b, int num_steps,
                double *const *snaps, int64_t ld_snaps, int snap_every, burg_stats *stats);
+/* The same sweep with the snapshot set left on the device: d_out is a
+ * C-order (2n x ld_out) matrix in device memory of the context's GPU, and
+ * trajectory j's num_steps / snap_every + 1 columns land at columns
+ * j * (num_steps / snap_every + 1) ... -- np.hstack of the per-mu matrices,
+ * the matrix C/run_prom.py:59-71 hands to POD (burg_pod_rsvd_device), with no
+ * host round trip.  Small grids run several trajectories side by side in one
+ * launch (either entry point). */
+int burg_sweep_device(burg_ctx *ctx, int nmu, const double *src_b, const double *lbc_b,
+                      int num_steps, int snap_every, double *d_out, int64_t ld_out,
+                      burg_stats *stats);
 
 /* One trajectory straight into a snapshot-cache file (load_or_compute_snaps'
  * compute-then-np.save, C/hypernet2D.py:3141-3143): the
@@ -383,6 +396,11 @@ int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *
  * All products are rocBLAS dgemm on the device. */
 int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
                   const double *omega, double *U, double *sigma, double *ms);
+/* burg_pod_rsvd (omega != NULL) or burg_pod (omega == NULL) on a snapshot
+ * matrix that is already in device memory of `device` (C-order m x ns, e.g.
+ * burg_sweep_device's): no upload.  U, sigma, omega are host arrays. */
+int burg_pod_rsvd_device(int device, int64_t m, int ns, const double *d_snaps, int k, int nrand,
+                         int n_iter, const double *omega, double *U, double *sigma, double *ms);
 
 #ifdef __cplusplus
 }
