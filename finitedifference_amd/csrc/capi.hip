@@ -1985,6 +1985,9 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
         if (int e = burg_ctx_create(c->device, nx, G * ny_pad, &ch)) return e;
         ch->bat_nd = G;
         ch->bat_ny_d = ny;
+        // (A/B knob: the stacked grid's tile target -- e.g. 4096 lets it take
+        // W = 8 tiles, two workgroups on some CUs)
+        if (const char *e = std::getenv("BURG_SWEEP_BATCH_TILES")) ch->tiles_target_opt = std::atoi(e);
         c->bat_child = ch;
         c->bat_child_G = G;
     }

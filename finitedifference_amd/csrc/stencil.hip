@@ -320,10 +320,13 @@ int residual_partials_count(const Coeffs &cf)
 }
 
 // Stencil variant (A/B knob BURG_STENCIL, bits: 1 XCD-aware block order, 2
-// next-row prefetch; default kStencilDefault).  Every variant computes the
-// same cells with the same op order: the results are bit-identical.
+// next-row prefetch).  Every variant computes the same cells with the same op
+// order: the results are bit-identical.  Measured at 8192^2 (round 4,
+// profiles/r04/stencil_ab_v1): residual 0.635 / 0.636 / 0.640 / 0.640 ms,
+// J.x 0.624 / 0.625 / 0.622 / 0.626 ms for variants 0 / 1 / 2 / 3 -- neither
+// helps, so the default is 0.
 #ifndef BURG_STENCIL_DEFAULT
-#define BURG_STENCIL_DEFAULT 3
+#define BURG_STENCIL_DEFAULT 0
 #endif
 int stencil_variant()
 {
