@@ -111,6 +111,12 @@ constexpr int kSL = 16;   // comm lanes per compute wave for the south / north s
 #ifndef BURG_NARROW_U
 #define BURG_NARROW_U 8
 #endif
+// steady-edge diagonals, round 4: one lane-compare per diagonal instead of two
+// (atE from the next diagonal's at0) and the narrow tiles' column-0 source +
+// inlet sum once per block (A/B knob: 0 = the round-3 code)
+#ifndef BURG_SE_OPT
+#define BURG_SE_OPT 1
+#endif
 // the comm wave's poll window (diagonals ahead of a compute wave's progress):
 // at least two blocks, so the next block's inflows arrive during this one
 template <int W>
@@ -173,7 +179,7 @@ template <int W>
 constexpr int la_of() { return u16_of<W>() ? 32 : BURG_KLA; }
 // LDS ring slots (steps) of the intra-workgroup west -> east edges
 template <int W>
-constexpr int rl_of() { return u16_of<W>() ? 2 : kPipeRL; }
+constexpr int rl_of() { return (u16_of<W>() || (W <= 16 && BURG_NARROW_U >= 16)) ? 2 : kPipeRL; }
 
 // s_waitcnt vmcnt(N) with expcnt / lgkmcnt at their maximum (no wait): gfx9
 // encoding vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt[5:4] << 14.  A
@@ -881,6 +887,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     // branch), and the inlet term added at column 0 (0 off the inlet tile)
     unsigned nv1 = kOOB, nv2 = kOOB;
     double lb_se = 0.0;
+    // narrow steady-edge blocks (BURG_SE_OPT): the column-0 source plus the
+    // inlet term, added once per block (the diagonal selects it at column 0)
+    double src0_se = 0.0;
     // a column's {hx, src}; sweeps take src from their per-trajectory tables,
     // so they load hx alone (a dead src half would be a register the compiler
     // reuses while the load is in flight: an LDS wait per diagonal)
@@ -1045,7 +1054,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const int q = t >> LW;
         const bool valid = STEADY || (unsigned)t < (unsigned)KW;
         const bool at0 = SE ? u == se_uw : EDGE & (c == 0);
-        const bool atE = SE ? u == se_ue : EDGE & (c == W - 1);
+        // (a lane reaches column W-1 one diagonal before column 0: with U < W
+        // the compare of diagonal u + 1's at0 serves as this one's atE)
+        const bool atE = SE ? ((BURG_SE_OPT && U < W) ? u + 1 == se_uw : u == se_ue)
+                            : EDGE & (c == W - 1);
         const bool need_w = has_west & at0 & valid & rowok;
         const bool need_s = has_south & (STEADY || s < KW);  // wave-uniform (lane 0 consumes)
         const bool out_e = atE & valid & rowok;
@@ -1061,7 +1073,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const double srcc = SWEEP ? in.src : co.y;
             // (narrow steady edge: srcc + 0.0 is srcc exactly -- the source
             // term is positive -- so both forms give the same bits)
-            const double sl = (!WIDE && STEADY) ? srcc + (at0 ? lb_se : 0.0)
+            const double sl = (!WIDE && STEADY) ? (BURG_SE_OPT ? (at0 ? src0_se : srcc)
+                                                              : srcc + (at0 ? lb_se : 0.0))
                                                 : (col0_tile && at0) ? srcc + lbu : srcc;
             p.hx = hx;
             const double hu = 0.5 * pu;
@@ -1222,7 +1235,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             int se_qw = 0;
             bool se_in = false;
             if constexpr (decltype(tag)::value >= 3) {
-                if constexpr (!WIDE) lb_se = col0_tile ? lb : 0.0;  // (no switch inside)
+                if constexpr (!WIDE) {
+                    lb_se = col0_tile ? lb : 0.0;  // (no switch inside)
+                    // the same sum the diagonal at column 0 would form:
+                    // src + lb_se (+ 0.0 off the inlet tile: src > 0, exact)
+                    src0_se = (SWEEP ? src_cur[0] : as_d2(sm.cc[k][0]).y) + lb_se;
+                }
                 // the lane's column-0 and column-(W-1) cells in this block
                 const int c0 = (sb - lane) & (W - 1);
                 se_uw = (W - c0) & (W - 1);
