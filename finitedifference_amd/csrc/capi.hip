@@ -247,7 +247,9 @@ int ensure_scratch(burg_ctx *c)
     if (int e = dalloc(&c->d_d, c->m())) return e;
     if (int e = dalloc(&c->d_x, c->m())) return e;
     c->npartials = residual_partials_count(c->cf);
-    if (int e = dalloc(&c->d_partials, (size_t)c->npartials)) return e;
+    // (+ one slot: the fused final sum's ticket counter, zero between launches)
+    if (int e = dalloc(&c->d_partials, (size_t)c->npartials + 1)) return e;
+    HIPCHK(hipMemsetAsync(c->d_partials + c->npartials, 0, sizeof(double), c->stream));
     if (int e = dalloc(&c->d_sumsq, 1)) return e;
     return 0;
 }

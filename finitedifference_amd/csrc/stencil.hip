@@ -79,7 +79,8 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
                                                           double *__restrict__ partials,
                                                           const double *__restrict__ halo_w,
                                                           const double *__restrict__ halo_wp,
-                                                          int rows, int nbx, int nb)
+                                                          int rows, int nbx, int nb,
+                                                          double *__restrict__ sumsq)
 {
     int bx, by;
     block_of<XCD>(nbx, nb, bx, by);
@@ -171,217 +172,38 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
         has_s = true;
     }
     block_sumsq(sq, partials + (size_t)by * nbx + bx);
-}
-
-// Two columns per thread (even nx; BURG_STENCIL bit 4): 16-B loads and
-// stores of the column pair (2c, 2c+1) -- half the memory instructions of
-// the one-column kernels for the same bytes.  Cell B's west terms are cell
-// A's (same thread); cell A's are the left thread's cell B (DPP), lane 0's
-// from its own loads of column 2c-1.  Same per-cell expressions as above, so
-// the residual / J.x are bit-identical; only the per-block sum of squares
-// (the norm's summation order) differs.
-typedef double dv2 __attribute__((ext_vector_type(2)));
-
-__global__ __launch_bounds__(kBlock) void residual2_kernel(Coeffs cf, const double *__restrict__ w,
-                                                           const double *__restrict__ wp,
-                                                           double *__restrict__ res,
-                                                           double *__restrict__ partials,
-                                                           const double *__restrict__ halo_w,
-                                                           const double *__restrict__ halo_wp,
-                                                           int rows, int nbx)
-{
-    const int by = blockIdx.x / nbx, bx = blockIdx.x - by * nbx;
-    const int nx = cf.nx, ny = cf.ny;
-    const size_t n = (size_t)nx * ny;
-    const int c = 2 * (bx * kBlock + (int)threadIdx.x);  // column of cell A; B = c + 1
-    const int r0 = by * rows;
-    const int r1 = min(ny, r0 + rows);
-    const bool colok = c < nx;
-    const int cc = colok ? c : nx - 2;
-    const bool lw = ((threadIdx.x & (kWave - 1)) == 0) && cc > 0;
-    const bool west = c > 0;
-    const double a = cf.alpha;
-    const double idxA = cf.inv_dx[cc], idxB = cf.inv_dx[cc + 1];
-    const double axA = a * idxA, axB = a * idxB;
-    const double idxw = west ? cf.inv_dx[cc - 1] : 0.0;
-    const double axw = a * idxw;
-    const double srcA = cf.src[cc], srcB = cf.src[cc + 1];
-    const double *u = w, *v = w + n, *up = wp, *vp = wp + n;
-
-    bool has_s = false;
-    double SvSA = 0.0, SuvSA = 0.0, SvSB = 0.0, SuvSB = 0.0, ays = 0.0;
-    if (r0 > 0 || halo_w != nullptr) {
-        dv2 uS, vS, upS, vpS;
-        if (r0 > 0) {
-            const size_t j = (size_t)(r0 - 1) * nx + cc;
-            uS = *(const dv2 *)&u[j], vS = *(const dv2 *)&v[j];
-            upS = *(const dv2 *)&up[j], vpS = *(const dv2 *)&vp[j];
-        } else {
-            uS = dv2{halo_w[cc], halo_w[cc + 1]}, vS = dv2{halo_w[nx + cc], halo_w[nx + cc + 1]};
-            upS = dv2{halo_wp[cc], halo_wp[cc + 1]};
-            vpS = dv2{halo_wp[nx + cc], halo_wp[nx + cc + 1]};
-        }
-        ays = a * cf.inv_dy[r0 - 1];
-        SvSA = 0.5 * (vS.x * vS.x) + 0.5 * (vpS.x * vpS.x);
-        SuvSA = (0.5 * uS.x) * vS.x + (0.5 * upS.x) * vpS.x;
-        SvSB = 0.5 * (vS.y * vS.y) + 0.5 * (vpS.y * vpS.y);
-        SuvSB = (0.5 * uS.y) * vS.y + (0.5 * upS.y) * vpS.y;
-        has_s = true;
+    if (sumsq == nullptr) return;
+    // The norm's final sum, fused (no second launch): the last block to
+    // finish sums the nb partials in index order, exactly as
+    // sum_partials_kernel does (the same bits).  Producer: each block's thread
+    // 0 stored its partial, then releases at agent scope before taking a
+    // ticket; the last block acquires and reads the partials at agent scope
+    // (other XCDs' L2s are not coherent with this one, MI355X_MICROARCH.md).
+    // The ticket lives just past the partials and is reset by the last block.
+    unsigned *ticket = (unsigned *)(partials + nb);
+    __shared__ int last;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        last = t + 1 == (unsigned)nb;
     }
-    double sq = 0.0;
-    for (int r = r0; r < r1; ++r) {
-        const size_t i = (size_t)r * nx + cc;
-        const dv2 U = *(const dv2 *)&u[i], V = *(const dv2 *)&v[i];
-        const dv2 UP = *(const dv2 *)&up[i], VP = *(const dv2 *)&vp[i];
-        double SuW0 = 0.0, SuvW0 = 0.0;
-        if (lw) {
-            const size_t j = i - 1;
-            const double uj = u[j], vj = v[j], upj = up[j], vpj = vp[j];
-            SuW0 = 0.5 * (uj * uj) + 0.5 * (upj * upj);
-            SuvW0 = (0.5 * uj) * vj + (0.5 * upj) * vpj;
-        }
-        const double ay = a * cf.inv_dy[r];
-        const double SuA = 0.5 * (U.x * U.x) + 0.5 * (UP.x * UP.x);
-        const double SvA = 0.5 * (V.x * V.x) + 0.5 * (VP.x * VP.x);
-        const double SuvA = (0.5 * U.x) * V.x + (0.5 * UP.x) * VP.x;
-        const double SuB = 0.5 * (U.y * U.y) + 0.5 * (UP.y * UP.y);
-        const double SvB = 0.5 * (V.y * V.y) + 0.5 * (VP.y * VP.y);
-        const double SuvB = (0.5 * U.y) * V.y + (0.5 * UP.y) * VP.y;
-        const double SuW = wave_shr1(SuW0, SuB);
-        const double SuvW = wave_shr1(SuvW0, SuvB);
-        // cell A (column c)
-        double dxu = axA * SuA, dyuv = ay * SuvA, dyv = ay * SvA, dxuv = idxA * SuvA;
-        if (west) {
-            dxu = dxu + (-axw) * SuW;
-            dxuv = dxuv + (-idxw) * SuvW;
-        }
-        if (has_s) {
-            dyuv = dyuv + (-ays) * SuvSA;
-            dyv = dyv + (-ays) * SvSA;
-        }
-        double ruA = U.x - UP.x;
-        ruA = ruA + dxu;
-        ruA = ruA + dyuv;
-        ruA = ruA - srcA;
-        ruA = ruA - (c == 0 ? cf.lbc[r] : 0.0);
-        double rvA = V.x - VP.x;
-        rvA = rvA + dyv;
-        rvA = rvA + a * dxuv;
-        // cell B (column c + 1): its west cell is A
-        double dxuB = axB * SuB, dyuvB = ay * SuvB, dyvB = ay * SvB, dxuvB = idxB * SuvB;
-        dxuB = dxuB + (-axA) * SuA;
-        dxuvB = dxuvB + (-idxA) * SuvA;
-        if (has_s) {
-            dyuvB = dyuvB + (-ays) * SuvSB;
-            dyvB = dyvB + (-ays) * SvSB;
-        }
-        double ruB = U.y - UP.y;
-        ruB = ruB + dxuB;
-        ruB = ruB + dyuvB;
-        ruB = ruB - srcB;
-        ruB = ruB - 0.0;
-        double rvB = V.y - VP.y;
-        rvB = rvB + dyvB;
-        rvB = rvB + a * dxuvB;
-        if (colok) {
-            __builtin_nontemporal_store(dv2{ruA, ruB}, (dv2 *)&res[i]);
-            __builtin_nontemporal_store(dv2{rvA, rvB}, (dv2 *)&res[n + i]);
-            sq += ruA * ruA + rvA * rvA;
-            sq += ruB * ruB + rvB * rvB;
-        }
-        SvSA = SvA;
-        SuvSA = SuvA;
-        SvSB = SvB;
-        SuvSB = SuvB;
-        ays = ay;
-        has_s = true;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nb; i += kBlock)
+        s += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ double red[kBlock];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = kBlock / 2; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
     }
-    block_sumsq(sq, partials + blockIdx.x);
-}
-
-__global__ __launch_bounds__(kBlock) void jvp2_kernel(Coeffs cf, const double *__restrict__ w,
-                                                      const double *__restrict__ x,
-                                                      double *__restrict__ y, int rows, int nbx)
-{
-    const int by = blockIdx.x / nbx, bx = blockIdx.x - by * nbx;
-    const int nx = cf.nx, ny = cf.ny;
-    const size_t n = (size_t)nx * ny;
-    const int c = 2 * (bx * kBlock + (int)threadIdx.x);
-    const int r0 = by * rows;
-    const int r1 = min(ny, r0 + rows);
-    const bool colok = c < nx;
-    const int cc = colok ? c : nx - 2;
-    const bool lw = ((threadIdx.x & (kWave - 1)) == 0) && cc > 0;
-    const bool west = c > 0;
-    const double a = cf.alpha;
-    const double axA = a * cf.inv_dx[cc], axB = a * cf.inv_dx[cc + 1];
-    const double axw = west ? a * cf.inv_dx[cc - 1] : 0.0;
-    const double *u = w, *v = w + n, *xu = x, *xv = x + n;
-
-    bool has_s = false;
-    double t2SA = 0.0, t3SA = 0.0, t2SB = 0.0, t3SB = 0.0;
-    if (r0 > 0) {
-        const size_t j = (size_t)(r0 - 1) * nx + cc;
-        const double ays = a * cf.inv_dy[r0 - 1];
-        const dv2 uS = *(const dv2 *)&u[j], vS = *(const dv2 *)&v[j];
-        const dv2 xuS = *(const dv2 *)&xu[j], xvS = *(const dv2 *)&xv[j];
-        const double mSA = vS.x * xuS.x + uS.x * xvS.x;
-        const double mSB = vS.y * xuS.y + uS.y * xvS.y;
-        t2SA = 0.5 * ays * mSA;
-        t3SA = ays * vS.x * xvS.x;
-        t2SB = 0.5 * ays * mSB;
-        t3SB = ays * vS.y * xvS.y;
-        has_s = true;
-    }
-    for (int r = r0; r < r1; ++r) {
-        const size_t i = (size_t)r * nx + cc;
-        const dv2 U = *(const dv2 *)&u[i], V = *(const dv2 *)&v[i];
-        const dv2 XU = *(const dv2 *)&xu[i], XV = *(const dv2 *)&xv[i];
-        double t1W0 = 0.0, t4W0 = 0.0;
-        if (lw) {
-            const size_t j = i - 1;
-            const double mW = v[j] * xu[j] + u[j] * xv[j];
-            t1W0 = axw * u[j] * xu[j];
-            t4W0 = 0.5 * axw * mW;
-        }
-        const double ay = a * cf.inv_dy[r];
-        const double mA = V.x * XU.x + U.x * XV.x;
-        const double t1A = axA * U.x * XU.x;
-        const double t2A = 0.5 * ay * mA;
-        const double t3A = ay * V.x * XV.x;
-        const double t4A = 0.5 * axA * mA;
-        const double mB = V.y * XU.y + U.y * XV.y;
-        const double t1B = axB * U.y * XU.y;
-        const double t2B = 0.5 * ay * mB;
-        const double t3B = ay * V.y * XV.y;
-        const double t4B = 0.5 * axB * mB;
-        const double t1W = wave_shr1(t1W0, t1B);
-        const double t4W = wave_shr1(t4W0, t4B);
-        double yuA = XU.x + t1A + t2A;
-        double yvA = XV.x + t3A + t4A;
-        if (west) {
-            yuA -= t1W;
-            yvA -= t4W;
-        }
-        double yuB = XU.y + t1B + t2B;
-        double yvB = XV.y + t3B + t4B;
-        yuB -= t1A;
-        yvB -= t4A;
-        if (has_s) {
-            yuA -= t2SA;
-            yvA -= t3SA;
-            yuB -= t2SB;
-            yvB -= t3SB;
-        }
-        if (colok) {
-            __builtin_nontemporal_store(dv2{yuA, yuB}, (dv2 *)&y[i]);
-            __builtin_nontemporal_store(dv2{yvA, yvB}, (dv2 *)&y[n + i]);
-        }
-        t2SA = t2A;
-        t3SA = t3A;
-        t2SB = t2B;
-        t3SB = t3B;
-        has_s = true;
+    if (threadIdx.x == 0) {
+        *sumsq = red[0];
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -516,12 +338,12 @@ __global__ __launch_bounds__(256) void transpose_kernel(StatePtrs sp, int nstate
 }  // namespace
 
 // Stencil variant (A/B knob BURG_STENCIL, bits: 1 XCD-aware block order, 2
-// next-row prefetch, 4 two columns per thread).  Every variant computes the
-// same cells with the same op order: the results are bit-identical (the
-// two-column kernels sum the norm's squares in another order).  Measured at
-// 8192^2 (round 4, profiles/r04/stencil_ab_v1): residual 0.635 / 0.636 /
-// 0.640 / 0.640 ms, J.x 0.624 / 0.625 / 0.622 / 0.626 ms for variants 0 / 1 /
-// 2 / 3 -- neither helps.
+// next-row prefetch).  Every variant computes the same cells with the same op
+// order: the results are bit-identical.  Measured at 8192^2 (round 4,
+// profiles/r04/stencil_ab_v1): residual 0.635 / 0.636 / 0.640 / 0.640 ms,
+// J.x 0.624 / 0.625 / 0.622 / 0.626 ms for variants 0 / 1 / 2 / 3 -- neither
+// helps.  (Two columns per thread with 16-B loads and stores were 23 % slower,
+// profiles/r04/stencil_ab_v2, and were removed.)
 #ifndef BURG_STENCIL_DEFAULT
 #define BURG_STENCIL_DEFAULT 0
 #endif
@@ -530,25 +352,29 @@ int stencil_variant()
     static int v = -1;
     if (v < 0) {
         v = BURG_STENCIL_DEFAULT;
-        if (const char *e = std::getenv("BURG_STENCIL")) v = std::atoi(e) & 7;
+        if (const char *e = std::getenv("BURG_STENCIL")) v = std::atoi(e) & 3;
     }
     return v;
 }
 
-// Block layout of the stencils: columns per thread (2 with BURG_STENCIL bit 4
-// and an even nx), column blocks, rows per block (enough blocks to fill the
-// chip, >= 2048; at most 64 rows -- carry reuse saturates long before).
+// Block layout of the stencils: column blocks of kBlock, rows per block
+// (enough blocks to fill the chip, >= 2048; at most 64 rows -- carry reuse
+// saturates long before; BURG_STENCIL_ROWS forces a power of two, A/B).
 struct StencilLayout {
-    int cpt, nbx, rows, nb;
+    int nbx, rows, nb;
 };
 static StencilLayout stencil_layout(const Coeffs &cf)
 {
+    static int force = -1;
+    if (force < 0) {
+        force = 0;
+        if (const char *e = std::getenv("BURG_STENCIL_ROWS")) force = std::atoi(e);
+    }
     StencilLayout l{};
-    l.cpt = ((stencil_variant() & 4) && cf.nx % 2 == 0) ? 2 : 1;
-    const int per = kBlock * l.cpt;
-    l.nbx = (cf.nx + per - 1) / per;
+    l.nbx = (cf.nx + kBlock - 1) / kBlock;
     l.rows = 64;
     while (l.rows > 4 && (long long)l.nbx * ((cf.ny + l.rows - 1) / l.rows) < 2048) l.rows >>= 1;
+    if (force >= 1 && force <= 1024) l.rows = force;
     l.nb = l.nbx * ((cf.ny + l.rows - 1) / l.rows);
     return l;
 }
@@ -561,17 +387,21 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
 {
     const StencilLayout l = stencil_layout(cf);
     const int rows = l.rows, nbx = l.nbx, nb = l.nb;
-    if (l.cpt == 2) {
-        residual2_kernel<<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx);
-    } else {
-        switch (stencil_variant() & 3) {
-        case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
-        case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
-        case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
-        default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
-        }
+    // the final sum fused into the last block (A/B knob BURG_SUMSQ_FUSED=0:
+    // the separate sum_partials_kernel launch of rounds 1-3)
+    static int fused = -1;
+    if (fused < 0) {
+        const char *e = std::getenv("BURG_SUMSQ_FUSED");
+        fused = e ? std::atoi(e) != 0 : 1;
     }
-    if (sumsq) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
+    double *fs = fused ? sumsq : nullptr;
+    switch (stencil_variant()) {
+    case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
+    case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
+    case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
+    default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
+    }
+    if (sumsq && !fused) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
@@ -579,15 +409,11 @@ int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y, hi
 {
     const StencilLayout l = stencil_layout(cf);
     const int rows = l.rows, nbx = l.nbx, nb = l.nb;
-    if (l.cpt == 2) {
-        jvp2_kernel<<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx);
-    } else {
-        switch (stencil_variant() & 3) {
-        case 0: jvp_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
-        case 1: jvp_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
-        case 2: jvp_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
-        default: jvp_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
-        }
+    switch (stencil_variant()) {
+    case 0: jvp_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    case 1: jvp_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    case 2: jvp_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
+    default: jvp_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
