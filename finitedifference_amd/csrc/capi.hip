@@ -1958,9 +1958,15 @@ int batch_group(burg_ctx *c, int nmu)
         return v >= 2 ? std::min({v, nmu, kBatchMax}) : 0;
     }
     if (c->stream_w_opt != 0 || c->tiles_target_opt != 0) return 0;
+    // only a grid that leaves at least half of the CUs idle (one workgroup
+    // per CU is the pipe engine's own plan; a grid that fills the chip, e.g.
+    // 1024^2, runs back to back in time, section 4.1c)
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess)
+        return 0;
     const int wgs = c->sp.nti * c->nwj;
     const int cap = pipe_max_resident_blocks(c->sp.W, false);
-    if (cap <= 0 || 2 * wgs > cap) return 0;
+    if (cap <= 0 || 2 * wgs > ncu) return 0;
     return std::min({nmu, cap / wgs, kBatchMax});
 }
 
