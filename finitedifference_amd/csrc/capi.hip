@@ -900,7 +900,12 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
                         "descriptor per tile (2 GiB); raise snap_every", n, W);
         const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
         const size_t need = (size_t)Lt * per_entry, have = c->ring_entries * sizeof(d2);
-        if (need > have) {
+        // a ring much larger than needed (one sized for the capped plain
+        // trajectory, ~240 GB) is given back and allocated to size: the
+        // windows at the start of the big allocation ran 17 % slower
+        // (16384 x 2048: 110 vs 94 ms per trajectory, profiles/r04/ring_pad_ab/
+        // ret_after_plain.json)
+        if (need > have || have > 2 * need + ((size_t)1 << 30)) {
             dfree(c->d_ring);
             c->ring_entries = 0;
             size_t freeb = 0, totalb = 0;
@@ -1993,8 +1998,12 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
         if (int e = burg_ctx_create(c->device, nx, G * ny_pad, &ch)) return e;
         ch->bat_nd = G;
         ch->bat_ny_d = ny;
-        // (A/B knob: the stacked grid's tile target -- e.g. 4096 lets it take
-        // W = 8 tiles, two workgroups on some CUs)
+        // The stacked grid's tile target: 4096 lets it take the narrowest
+        // tiles that stay resident (W = 8 at 9 x 250^2: 1 152 tiles, two
+        // workgroups on some CUs) -- 2.86 ms per 9-trajectory launch against
+        // 4.03 ms with W = 16 (profiles/r04/sweep250; back to back in time:
+        // 19.47 ms).  BURG_SWEEP_BATCH_TILES overrides (A/B knob).
+        ch->tiles_target_opt = 4096;
         if (const char *e = std::getenv("BURG_SWEEP_BATCH_TILES")) ch->tiles_target_opt = std::atoi(e);
         c->bat_child = ch;
         c->bat_child_G = G;
@@ -2023,6 +2032,12 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
         ch->ov_colc = nullptr;
         (void)hipStreamSynchronize(ch->stream);
         (void)hipStreamSynchronize(c->stream);
+        // the internal context's ring (G trajectories of states) is given back:
+        // the parent context may need the memory next
+        dfree(ch->d_ring);
+        ch->ring_entries = 0;
+        ch->ring_maxed = false;
+        ch->tr.valid = false;
         if (registered)
             for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(out.host[j]);
         dfree(d_srcb);
@@ -2058,7 +2073,10 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
                 break;
             if (out.host) {
                 size_t freeb = 0, totalb = 0;
-                HIPCHK(hipMemGetInfo(&freeb, &totalb));
+                if (hipMemGetInfo(&freeb, &totalb) != hipSuccess) {
+                    rc = fail(BURG_EHIP, "hipMemGetInfo failed");
+                    break;
+                }
                 S = (int)std::min<int64_t>(ncols, 64);
                 while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
                 if ((rc = dalloc(&d_tr, (size_t)S * m))) break;
@@ -2073,9 +2091,13 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
                     }
             }
         }
-        HIPCHK(hipMemcpyAsync(d_srcb, srcg.data(), sizeof(double) * G * nx, hipMemcpyHostToDevice,
-                              ch->stream));
-        CHK(launch_colc_batch(ch->cf, G, d_srcb, (int)ncolp, d_colcb, ch->stream));
+        if (hipMemcpyAsync(d_srcb, srcg.data(), sizeof(double) * G * nx, hipMemcpyHostToDevice,
+                           ch->stream) != hipSuccess ||
+            launch_colc_batch(ch->cf, G, d_srcb, (int)ncolp, d_colcb, ch->stream) != 0) {
+            rc = fail(BURG_EHIP, "side-by-side sweep: column tables: %s",
+                      hipGetErrorString(hipGetLastError()));
+            break;
+        }
         ch->bat_colc_stride = ncolp;
         ch->ov_colc = d_colcb;
         if ((rc = burg_upload_state(ch, w0s.data()))) break;

@@ -180,17 +180,23 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
     // ticket; the last block acquires and reads the partials at agent scope
     // (other XCDs' L2s are not coherent with this one, MI355X_MICROARCH.md).
     // The ticket lives just past the partials and is reset by the last block.
+    // (No fences: a release fence is an L2 write-back -- microseconds per
+    // block, round 4 measured the residual 0.70 -> 0.85 ms with one per block.
+    // Instead the partial is re-stored write-through at agent scope and
+    // drained before the ticket, and the last block reads the partials with
+    // agent-scope loads: MI355X_MICROARCH.md's sc1 form of the hand-off.)
     unsigned *ticket = (unsigned *)(partials + nb);
     __shared__ int last;
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        double *mine = partials + (size_t)by * nbx + bx;
+        __hip_atomic_store(mine, *mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_s_waitcnt(0);
         const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT);
         last = t + 1 == (unsigned)nb;
     }
     __syncthreads();
     if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     double s = 0.0;
     for (int i = threadIdx.x; i < nb; i += kBlock)
         s += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -392,7 +398,7 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
     static int fused = -1;
     if (fused < 0) {
         const char *e = std::getenv("BURG_SUMSQ_FUSED");
-        fused = e ? std::atoi(e) != 0 : 1;
+        fused = e ? std::atoi(e) != 0 : 0;
     }
     double *fs = fused ? sumsq : nullptr;
     switch (stencil_variant()) {
