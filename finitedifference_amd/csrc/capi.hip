@@ -893,7 +893,11 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
     *mp = TrajMap{};
     if (k >= 2 && c->eng_eff == BURG_ENGINE_PIPE && (long long)k * W >= W + 64) {
         const int n = num_steps / k;
-        const long long Lw = 2LL * W + 128;  // a multiple of every block length
+        // working ring: 2W + 128 entries (a multiple of every block length);
+        // BURG_RET_LW=m makes it m W + 128 (A/B knob)
+        long long lwm = 2;
+        if (const char *e = std::getenv("BURG_RET_LW")) lwm = std::max(2LL, std::atoll(e));
+        const long long Lw = lwm * W + 128;
         const long long Lt = ring_stride(Lw + (long long)n * (W + 64));
         if (Lt >= (1LL << 21))
             return fail(BURG_ESHAPE, "%d retained states of %d-wide tiles exceed one buffer "
