@@ -205,8 +205,6 @@ int launch_solve_pass(const Coeffs &cf, const Engine &eg, const double *w,
                       const double *rhs, double *delta, int pass, bool final,
                       DevStats *stats, hipStream_t st);
 
-// partials: residual_partials_count(cf) + 1 doubles (the last: the fused
-// final sum's ticket, zero-initialised by the caller)
 int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
                     double *partials, double *sumsq, const double *halo_w,
                     const double *halo_wp, hipStream_t st);

@@ -247,9 +247,7 @@ int ensure_scratch(burg_ctx *c)
     if (int e = dalloc(&c->d_d, c->m())) return e;
     if (int e = dalloc(&c->d_x, c->m())) return e;
     c->npartials = residual_partials_count(c->cf);
-    // (+ one slot: the fused final sum's ticket counter, zero between launches)
-    if (int e = dalloc(&c->d_partials, (size_t)c->npartials + 1)) return e;
-    HIPCHK(hipMemsetAsync(c->d_partials + c->npartials, 0, sizeof(double), c->stream));
+    if (int e = dalloc(&c->d_partials, (size_t)c->npartials)) return e;
     if (int e = dalloc(&c->d_sumsq, 1)) return e;
     return 0;
 }
@@ -918,7 +916,17 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
                 return fail(BURG_ENOMEM, "%d retained states (%.1f GB) do not fit in HBM; raise "
                             "snap_every", n, (double)need / 1e9);
         }
-        if (int e = ensure_ring(c, Lt)) return e;
+        {
+            // A/B knob BURG_RET_ALLOC_GB: allocate at least this much ring
+            // (does the allocation's size change where -- and how fast -- it
+            // lands?)
+            long long Lalloc = Lt;
+            if (const char *e = std::getenv("BURG_RET_ALLOC_GB")) {
+                const double gb = std::atof(e);
+                if (gb > 0) Lalloc = std::max<long long>(Lt, (long long)(gb * 1e9 / (double)per_entry));
+            }
+            if (int e = ensure_ring(c, Lalloc)) return e;
+        }
         if (!c->d_ret0)
             if (int e = dalloc(&c->d_ret0, c->m())) return e;
         mp->L = Lw;

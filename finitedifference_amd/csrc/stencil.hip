@@ -79,8 +79,7 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
                                                           double *__restrict__ partials,
                                                           const double *__restrict__ halo_w,
                                                           const double *__restrict__ halo_wp,
-                                                          int rows, int nbx, int nb,
-                                                          double *__restrict__ sumsq)
+                                                          int rows, int nbx, int nb)
 {
     int bx, by;
     block_of<XCD>(nbx, nb, bx, by);
@@ -172,45 +171,6 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
         has_s = true;
     }
     block_sumsq(sq, partials + (size_t)by * nbx + bx);
-    if (sumsq == nullptr) return;
-    // The norm's final sum, fused (no second launch): the last block to
-    // finish sums the nb partials in index order, exactly as
-    // sum_partials_kernel does (the same bits).  Producer: each block's thread
-    // 0 stored its partial, then releases at agent scope before taking a
-    // ticket; the last block acquires and reads the partials at agent scope
-    // (other XCDs' L2s are not coherent with this one, MI355X_MICROARCH.md).
-    // The ticket lives just past the partials and is reset by the last block.
-    // (No fences: a release fence is an L2 write-back -- microseconds per
-    // block, round 4 measured the residual 0.70 -> 0.85 ms with one per block.
-    // Instead the partial is re-stored write-through at agent scope and
-    // drained before the ticket, and the last block reads the partials with
-    // agent-scope loads: MI355X_MICROARCH.md's sc1 form of the hand-off.)
-    unsigned *ticket = (unsigned *)(partials + nb);
-    __shared__ int last;
-    if (threadIdx.x == 0) {
-        double *mine = partials + (size_t)by * nbx + bx;
-        __hip_atomic_store(mine, *mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_s_waitcnt(0);
-        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        last = t + 1 == (unsigned)nb;
-    }
-    __syncthreads();
-    if (!last) return;
-    double s = 0.0;
-    for (int i = threadIdx.x; i < nb; i += kBlock)
-        s += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __shared__ double red[kBlock];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = kBlock / 2; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) {
-        *sumsq = red[0];
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 }
 
 __global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double *partials, int np,
@@ -363,9 +323,15 @@ int stencil_variant()
     return v;
 }
 
-// Block layout of the stencils: column blocks of kBlock, rows per block
-// (enough blocks to fill the chip, >= 2048; at most 64 rows -- carry reuse
-// saturates long before; BURG_STENCIL_ROWS forces a power of two, A/B).
+// Block layout of the stencils: column blocks of kBlock, rows per block: the
+// tallest block (<= 64 rows) that still gives >= 16384 blocks, down to 8 rows.
+// Round 4 (profiles/r04/stencil_ab_v3 .. v5, one box each): at 8192^2 the
+// residual / J.x took 0.683 / 0.668 ms with 64-row blocks (4096 blocks, the
+// rounds 1-3 rule), 0.625 / 0.603 with 32, 0.625 / 0.593 with 16, 0.654 /
+// 0.595 with 8; at 4096^2 8 rows were best (0.177 / 0.159 ms).  More, shorter
+// blocks keep more of them in flight per CU through the grid's tail; the
+// south-row re-read they add (1 row in 16) costs less.  BURG_STENCIL_ROWS
+// forces a height (A/B knob).
 struct StencilLayout {
     int nbx, rows, nb;
 };
@@ -379,7 +345,7 @@ static StencilLayout stencil_layout(const Coeffs &cf)
     StencilLayout l{};
     l.nbx = (cf.nx + kBlock - 1) / kBlock;
     l.rows = 64;
-    while (l.rows > 4 && (long long)l.nbx * ((cf.ny + l.rows - 1) / l.rows) < 2048) l.rows >>= 1;
+    while (l.rows > 8 && (long long)l.nbx * ((cf.ny + l.rows - 1) / l.rows) < 16384) l.rows >>= 1;
     if (force >= 1 && force <= 1024) l.rows = force;
     l.nb = l.nbx * ((cf.ny + l.rows - 1) / l.rows);
     return l;
@@ -393,21 +359,16 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
 {
     const StencilLayout l = stencil_layout(cf);
     const int rows = l.rows, nbx = l.nbx, nb = l.nb;
-    // the final sum fused into the last block (A/B knob BURG_SUMSQ_FUSED=0:
-    // the separate sum_partials_kernel launch of rounds 1-3)
-    static int fused = -1;
-    if (fused < 0) {
-        const char *e = std::getenv("BURG_SUMSQ_FUSED");
-        fused = e ? std::atoi(e) != 0 : 0;
-    }
-    double *fs = fused ? sumsq : nullptr;
+    // (round 4: the final sum fused into the last block -- an agent-scope
+    // ticket, sc1 partials -- measured the same as this second launch,
+    // profiles/r04/stencil_ab_v4, and was not kept)
     switch (stencil_variant()) {
-    case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
-    case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
-    case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
-    default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb, fs); break;
+    case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
+    default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
     }
-    if (sumsq && !fused) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
+    if (sumsq) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
