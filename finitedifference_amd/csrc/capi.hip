@@ -891,42 +891,41 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
     *mp = TrajMap{};
     if (k >= 2 && c->eng_eff == BURG_ENGINE_PIPE && (long long)k * W >= W + 64) {
         const int n = num_steps / k;
-        // working ring: 2W + 128 entries (a multiple of every block length);
-        // BURG_RET_LW=m makes it m W + 128 (A/B knob)
-        long long lwm = 2;
-        if (const char *e = std::getenv("BURG_RET_LW")) lwm = std::max(2LL, std::atoll(e));
-        const long long Lw = lwm * W + 128;
-        const long long Lt = ring_stride(Lw + (long long)n * (W + 64));
-        if (Lt >= (1LL << 21))
-            return fail(BURG_ESHAPE, "%d retained states of %d-wide tiles exceed one buffer "
-                        "descriptor per tile (2 GiB); raise snap_every", n, W);
         const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
-        const size_t need = (size_t)Lt * per_entry, have = c->ring_entries * sizeof(d2);
-        // a ring much larger than needed (one sized for the capped plain
-        // trajectory, ~240 GB) is given back and allocated to size: the
-        // windows at the start of the big allocation ran 17 % slower
-        // (16384 x 2048: 110 vs 94 ms per trajectory, profiles/r04/ring_pad_ab/
-        // ret_after_plain.json)
-        if (need > have || have > 2 * need + ((size_t)1 << 30)) {
+        const long long Lwin = (long long)n * (W + 64);
+        const size_t have = c->ring_entries * sizeof(d2);
+        size_t freeb = 0, totalb = 0;
+        HIPCHK(hipMemGetInfo(&freeb, &totalb));
+        const size_t avail = (freeb + have) / 100 * 85;
+        const size_t ret0 = c->d_ret0 ? 0 : c->m() * sizeof(double);
+        // The working ring: as long as the memory budget allows, up to the
+        // whole trajectory's diagonals -- each tile then walks a long region
+        // of its ring as the plain ring does.  (Round 4: with a short working
+        // ring of 2W + 128 entries the windowed trajectory ran 93-95 ms on
+        // some boxes and allocations and 110-112 ms on others, while the
+        // plain capped ring held 93-95 ms everywhere, profiles/r04/
+        // ret_variance.)  At least 2W + 128 entries, a multiple of every block
+        // length.  BURG_RET_LW=m: exactly m W + 128 (A/B knob).
+        long long Lw = (long long)num_steps * W + W + 96;
+        const long long Lmem = avail > ret0 ? (long long)((avail - ret0) / per_entry) - Lwin - 2 : 0;
+        Lw = std::min(Lw, Lmem);
+        Lw = std::min(Lw, (1LL << 21) - 2 - Lwin);
+        Lw = Lw / 16 * 16;
+        if (const char *e = std::getenv("BURG_RET_LW")) Lw = std::max(2LL, std::atoll(e)) * W + 128;
+        if (Lw < 2LL * W + 128) {
+            if (Lwin + 2LL * W + 128 >= (1LL << 21))
+                return fail(BURG_ESHAPE, "%d retained states of %d-wide tiles exceed one buffer "
+                            "descriptor per tile (2 GiB); raise snap_every", n, W);
+            return fail(BURG_ENOMEM, "%d retained states (%.1f GB) do not fit in HBM; raise "
+                        "snap_every", n, (double)(Lwin + 2LL * W + 128) * per_entry / 1e9);
+        }
+        const long long Lt = ring_stride(Lw + Lwin);
+        const size_t need = (size_t)Lt * per_entry;
+        if (need > have || have > need + need / 4 + ((size_t)1 << 30)) {
             dfree(c->d_ring);
             c->ring_entries = 0;
-            size_t freeb = 0, totalb = 0;
-            HIPCHK(hipMemGetInfo(&freeb, &totalb));
-            if (need + c->m() * sizeof(double) > freeb / 100 * 85)
-                return fail(BURG_ENOMEM, "%d retained states (%.1f GB) do not fit in HBM; raise "
-                            "snap_every", n, (double)need / 1e9);
         }
-        {
-            // A/B knob BURG_RET_ALLOC_GB: allocate at least this much ring
-            // (does the allocation's size change where -- and how fast -- it
-            // lands?)
-            long long Lalloc = Lt;
-            if (const char *e = std::getenv("BURG_RET_ALLOC_GB")) {
-                const double gb = std::atof(e);
-                if (gb > 0) Lalloc = std::max<long long>(Lt, (long long)(gb * 1e9 / (double)per_entry));
-            }
-            if (int e = ensure_ring(c, Lalloc)) return e;
-        }
+        if (int e = ensure_ring(c, Lt)) return e;
         if (!c->d_ret0)
             if (int e = dalloc(&c->d_ret0, c->m())) return e;
         mp->L = Lw;

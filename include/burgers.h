@@ -270,7 +270,8 @@ int burg_reserve_trajectory(burg_ctx *ctx, int num_steps);
 /* What burg_trajectory_ex(ctx, num_steps, snap_every) would keep, without
  * allocating: the resolved snap_every (auto -> 1 or 10), the number of
  * retained states (-1: a capped ring, known after the run) and the ring's
- * bytes (0 when capped). */
+ * minimum bytes (0 when capped; a windowed ring's working part then grows to
+ * the memory budget). */
 int burg_trajectory_plan(burg_ctx *ctx, int num_steps, int snap_every, int *snap_every_out,
                          int64_t *retained_states, int64_t *ring_bytes);
 /* The states the last burg_trajectory_ex keeps resident: first_state,
