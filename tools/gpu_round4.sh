@@ -23,7 +23,7 @@ grep '"halo_fallback": "device' $O/bench_rehearse_fallback.json > /dev/null || {
 BURG_SPIN_SECONDS=3 BURG_TEST_FAIL_DEVICE_HALO=1:3 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 2 --rehearse-one-gpu --nx 2048 --rows-per-gpu 1024 --stream-w 128 --steps 5 --warmup 1 --no-alone > $O/bench_rehearse_failone.json 2> $O/bench_rehearse_failone.err || { tail -20 $O/bench_rehearse_failone.err; exit 1; }
 grep '"halo_fallback": "device' $O/bench_rehearse_failone.json > /dev/null || { echo "no fall-back recorded (fail-one)"; exit 1; }
 grep -h "bench.py rank" $O/bench_rehearse_failone.err | head -4
-TAG=${TAG:-r4_round}_mall bash tools/probes/mall_probe.sh || exit 1
+[ -n "$NO_MALL" ] || TAG=${TAG:-r4_round}_mall bash tools/probes/mall_probe.sh || exit 1
 if [ "$AB" = "1" ]; then
   TAG=${TAG:-r4_round}_ab TESTLIB=$TESTLIB LIBS="$LIBS" bash tools/probes/ab_both.sh || exit 1
 fi

@@ -23,6 +23,12 @@ BL="tools/lspg_probe.py 1024 95 3"
 S8="bench.py --nx 8192 --rows-per-gpu 2048 --steps 3 --warmup 1 --no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e --no-residual-check"
 S16="bench.py --nx 16384 --rows-per-gpu 2048 --steps 2 --warmup 1 --no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e --no-residual-check"
 for name in ${NAMES:-b4 b1 bs bl}; do
+  if [ "$name" = pod ]; then
+    # where the 250^2 rsvd POD's device time goes (kernel stats only)
+    POD_PROBE_RSVD_ONLY=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/pod_stats -o run -- python3 tools/pod_probe.py > $O/pod_probe.json 2> $O/pod_stats.err || { tail -5 $O/pod_stats.err; exit 1; }
+    echo "pod stats ok"
+    continue
+  fi
   case $name in b4) CMD=$B4;; b1) CMD=$B1;; bs) CMD=$BS;; bl) CMD=$BL;; s8) CMD=$S8;; s16) CMD=$S16;; esac
   if [ "$name" = s8 ] || [ "$name" = s16 ]; then
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${name}_stats -o run -- python3 $CMD > $O/${name}_bench.json 2> $O/${name}_stats.err || { tail -5 $O/${name}_stats.err; exit 1; }
