@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace burg {
 namespace {
@@ -147,11 +148,12 @@ int splitk_parts(rocblas_int m, rocblas_int n, rocblas_int k)
 // c = 11 (m R + R (R + 1)) u bounds ||Y||_2^2 <= trace(G) and keeps the
 // Cholesky factorisation of G + shift I from breaking down for any
 // cond(Y) < 1/u.  One workgroup.
-__global__ __launch_bounds__(kPB) void shift_diag_kernel(double *__restrict__ g, int r, double c)
+__global__ __launch_bounds__(kPB) void shift_diag_kernel(double *__restrict__ g, int r, double c,
+                                                         int ldg)
 {
     __shared__ double part[kPB];
     double t = 0.0;
-    for (int i = threadIdx.x; i < r; i += kPB) t += g[(size_t)i * r + i];
+    for (int i = threadIdx.x; i < r; i += kPB) t += g[(size_t)i * ldg + i];
     part[threadIdx.x] = t;
     __syncthreads();
     for (int h = kPB / 2; h > 0; h >>= 1) {
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(kPB) void shift_diag_kernel(double *__restrict__ g,
         __syncthreads();
     }
     const double shift = c * part[0];
-    for (int i = threadIdx.x; i < r; i += kPB) g[(size_t)i * r + i] += shift;
+    for (int i = threadIdx.x; i < r; i += kPB) g[(size_t)i * ldg + i] += shift;
 }
 
 // Orthonormal basis of the columns of Y (rows x r, column-major, in place):
@@ -183,7 +185,7 @@ rocblas_status orth_columns(rocblas_handle h, hipStream_t st, rocblas_int rows, 
         if ((s = gemm_tn_splitk(h, st, r, r, rows, y, rows, y, rows, g, r, work,
                                 splitk_parts(r, r, rows))) != rocblas_status_success)
             return s;
-        if (pass == 0) hipLaunchKernelGGL(shift_diag_kernel, dim3(1), dim3(kPB), 0, st, g, (int)r, c);
+        if (pass == 0) hipLaunchKernelGGL(shift_diag_kernel, dim3(1), dim3(kPB), 0, st, g, (int)r, c, (int)r);
         if ((s = rocsolver_dpotrf(h, rocblas_fill_upper, r, g, r, info)) != rocblas_status_success)
             return s;
         rocblas_int hinfo = 0;
@@ -203,7 +205,531 @@ rocblas_status orth_columns(rocblas_handle h, hipStream_t st, rocblas_int rows, 
     return rocblas_status_success;
 }
 
+// ---- Tall-skinny products on the matrix cores ------------------------------
+//
+// The randomized SVD's work is its 16 products with the (m x ns) snapshot
+// matrix S -- Y = S Z (m x R) and Z = S^T Y (ns x R), R = nrand = 105: 118
+// GFLOP each at 250^2 x 9 mu (125 000 x 4 509), 26 flop per byte of S, so
+// bound by the fp64 matrix rate (v_mfma_f64_16x16x4_f64; 78.6 TF/s peak, the
+// same as fp64 VALU FMA) rather than by HBM.  The kernels below use S as it
+// lies (C-order = row-major: no transposed copy), keep every thin operand
+// row-major with its columns padded with zeros to Rp = 16 NB <= 128, stage
+// the thin operand through LDS 32 reduction rows at a time (double-buffered,
+// one barrier per chunk; its next chunk and the next A operands are loaded
+// into registers before the MFMAs of the current one and stored to LDS
+// after them), and give every wave a 32 x Rp block of the output in
+// accumulators (2 x NB 16 x 16 tiles):
+//  * gemm_nn_kernel: C (m x n) = A (m x K) B (K x n); a workgroup owns 128
+//    rows of A (4 waves x 32) and the whole K reduction;
+//  * gemm_tn_kernel: W_p (K x Rp) = A_p^T B_p over row part p; a workgroup
+//    owns 128 columns of A and one part; sum_rows_kernel adds the parts in a
+//    fixed order (deterministic).  Parts map to XCDs (blockIdx mod 8) so
+//    that every column tile of a part runs on one XCD and reads B_p through
+//    that XCD's L2.
+// An MFMA's 4 k slots may carry any 4 reduction indices as long as A and B
+// agree: slot s4 = lane >> 4 takes k = 8 s4 + s in the s-th of the 8 MFMAs
+// of a chunk, so a lane's A operands of gemm_nn are 8 consecutive doubles of
+// one row of S, and gemm_tn's 16 lanes of a slot read 128 contiguous bytes.
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+constexpr int kTK = 32;   // reduction rows per chunk
+constexpr int kTW = 256;  // threads per workgroup (4 waves)
+
+struct TsArgs {
+    const double *a;  // row-major, row stride lda
+    const double *b;  // row-major (reduction x n), row stride ldb
+    double *c;        // nn: (m x n), row stride ldc; tn: parts x K x (16 NB) partials
+    size_t lda, ldb, ldc;
+    size_t m;         // rows of A (and of B for tn)
+    int K;            // nn: columns of A = rows of B; tn: columns of A = output rows
+    int n;            // valid columns of B and of the output
+    int jtiles;       // tn: column tiles of 128
+    size_t part_rows; // tn: rows per part
+};
+
+template <int NB>
+__device__ __forceinline__ void ts_mfma_chunk(const double *bs, int cl, int s4,
+                                              const double (&av)[2][8], dbl4 (&acc)[2][NB])
+{
+    constexpr int LDB = 16 * NB + 2;  // +2: the 4 k slots' rows start 8 rows = 16 banks apart
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+        const double *brow = bs + (8 * s4 + s) * LDB + cl;
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) {
+            const double bv = brow[16 * cb];
+            acc[0][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0][s], bv, acc[0][cb], 0, 0, 0);
+            acc[1][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1][s], bv, acc[1][cb], 0, 0, 0);
+        }
+    }
+}
+
+// this thread's share (2 NB doubles) of a kTK x 16 NB chunk of the thin
+// operand: rows r0 .. r0 + kTK - 1 (valid below r_end), columns below n
+template <int NB>
+__device__ __forceinline__ void ts_load_b(const TsArgs &g, size_t r0, size_t r_end,
+                                          double (&bn)[2 * NB])
+{
+    constexpr int NC = 16 * NB;
+#pragma unroll
+    for (int q = 0; q < 2 * NB; ++q) {
+        const int e = threadIdx.x + kTW * q;
+        const int kk = e / NC, cc = e % NC;
+        const size_t r = r0 + kk;
+        bn[q] = (r < r_end && cc < g.n) ? g.b[r * g.ldb + cc] : 0.0;
+    }
+}
+
+template <int NB>
+__device__ __forceinline__ void ts_store_b(double *bs, const double (&bn)[2 * NB])
+{
+    constexpr int NC = 16 * NB, LDB = NC + 2;
+#pragma unroll
+    for (int q = 0; q < 2 * NB; ++q) {
+        const int e = threadIdx.x + kTW * q;
+        bs[(e / NC) * LDB + e % NC] = bn[q];
+    }
+}
+
+template <int NB>
+__global__ __launch_bounds__(kTW) void gemm_nn_kernel(TsArgs g)
+{
+    constexpr int LDB = 16 * NB + 2;
+    __shared__ double bs[2][kTK * LDB];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane & 15, s4 = lane >> 4;
+    const size_t row0 = (size_t)blockIdx.x * 128 + (size_t)w * 32;
+    const double *ap[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+        const size_t r = row0 + 16 * rb + cl;
+        ap[rb] = g.a + (r < g.m ? r : g.m - 1) * g.lda;  // rows past m: results dropped
+    }
+    dbl4 acc[2][NB];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[rb][cb] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int nch = (g.K + kTK - 1) / kTK;
+    double av[2][8], an[2][8], bn[2 * NB];
+    auto load_a = [&](int ch) {
+        const int k0 = ch * kTK + 8 * s4;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) an[rb][s] = k0 + s < g.K ? ap[rb][k0 + s] : 0.0;
+    };
+    load_a(0);
+    ts_load_b<NB>(g, 0, (size_t)g.K, bn);
+    ts_store_b<NB>(bs[0], bn);
+    for (int ch = 0; ch < nch; ++ch) {
+        __syncthreads();
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
+        const bool more = ch + 1 < nch;
+        if (more) {
+            load_a(ch + 1);
+            ts_load_b<NB>(g, (size_t)(ch + 1) * kTK, (size_t)g.K, bn);
+        }
+        ts_mfma_chunk<NB>(bs[ch & 1], cl, s4, av, acc);
+        if (more) ts_store_b<NB>(bs[(ch + 1) & 1], bn);
+    }
+    // D layout of the f64 MFMA: column lane & 15, row (lane >> 4) + 4 q
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const size_t r = row0 + 16 * rb + s4 + 4 * q;
+                const int col = 16 * cb + cl;
+                if (r < g.m && col < g.n) g.c[r * g.ldc + col] = acc[rb][cb][q];
+            }
+}
+
+template <int NB>
+__global__ __launch_bounds__(kTW) void gemm_tn_kernel(TsArgs g)
+{
+    constexpr int NC = 16 * NB, LDB = NC + 2;
+    __shared__ double bs[2][kTK * LDB];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cl = lane & 15, s4 = lane >> 4;
+    const int x = blockIdx.x & 7, q8 = blockIdx.x >> 3;
+    const int p = x + 8 * (q8 / g.jtiles), jt = q8 % g.jtiles;
+    const size_t i_beg = std::min(g.m, (size_t)p * g.part_rows);
+    const size_t i_end = std::min(g.m, i_beg + g.part_rows);
+    const int j0 = jt * 128 + w * 32;
+    const double *ap[2];
+    bool jok[2];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+        const int j = j0 + 16 * rb + cl;
+        jok[rb] = j < g.K;
+        ap[rb] = g.a + (jok[rb] ? j : 0);
+    }
+    dbl4 acc[2][NB];
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb) acc[rb][cb] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int nch = (int)((i_end - i_beg + kTK - 1) / kTK);
+    double av[2][8], an[2][8], bn[2 * NB];
+    auto load_a = [&](int ch) {
+        const size_t i0 = i_beg + (size_t)ch * kTK + 8 * s4;
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+                an[rb][s] = (jok[rb] && i0 + s < i_end) ? ap[rb][(i0 + s) * g.lda] : 0.0;
+    };
+    if (nch > 0) {
+        load_a(0);
+        ts_load_b<NB>(g, i_beg, i_end, bn);
+        ts_store_b<NB>(bs[0], bn);
+    }
+    for (int ch = 0; ch < nch; ++ch) {
+        __syncthreads();
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
+        const bool more = ch + 1 < nch;
+        if (more) {
+            load_a(ch + 1);
+            ts_load_b<NB>(g, i_beg + (size_t)(ch + 1) * kTK, i_end, bn);
+        }
+        ts_mfma_chunk<NB>(bs[ch & 1], cl, s4, av, acc);
+        if (more) ts_store_b<NB>(bs[(ch + 1) & 1], bn);
+    }
+    double *wp = g.c + (size_t)p * g.K * NC;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < NB; ++cb)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int j = j0 + 16 * rb + s4 + 4 * q;
+                if (j < g.K) wp[(size_t)j * NC + 16 * cb + cl] = acc[rb][cb][q];
+            }
+}
+
+// out (K x n, row stride ldo) = sum over p < parts of W[p] (K x nc packed), in order
+__global__ __launch_bounds__(kPB) void sum_rows_kernel(const double *__restrict__ w, int parts,
+                                                       int K, int nc, int n,
+                                                       double *__restrict__ out, int ldo)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= (size_t)K * n) return;
+    const size_t j = e / n, c = e % n;
+    const size_t kn = (size_t)K * nc;
+    double t = 0.0;
+    for (int p = 0; p < parts; ++p) t += w[p * kn + j * nc + c];
+    out[j * ldo + c] = t;
+}
+
+// SVD of a small square matrix M (R x R, R <= 128) in one workgroup: one-sided
+// Jacobi (Hestenes) on the columns of M held column-major in LDS -- cyclic
+// round-robin sweeps, R/2 disjoint column pairs per step (16 waves, a pair
+// per wave at a time, rows over the lanes), each pair rotated until
+// |a_p . a_q| <= sqrt(R) eps ||a_p|| ||a_q||; then sigma_j = ||a_j|| and
+// u_j = a_j / sigma_j, sorted by decreasing sigma.  Relative accuracy for
+// every singular value (no bidiagonalisation): the small SVD of the
+// randomized SVD (B = Q^T S) after B^T = Q_b R_b, replacing rocSOLVER's
+// dgesvd of the wide 105 x 4 509 B (bidiagonalisation with one gemv pair per
+// column and ~360 bdsqr launches: ~50 ms of the 250^2 POD).
+// In: M[i][j] = src[j * lds + i] (column j of M = row j of a row-major
+// source).  Out: U (R x R column-major, ld R), sigma (R), info (0, or 1 if
+// the sweeps did not converge).
+constexpr int kJT = 1024;
+constexpr int kJacMaxSweeps = 60;
+__global__ __launch_bounds__(kJT) void jacobi_svd_kernel(const double *__restrict__ src, int lds,
+                                                         int R, double *__restrict__ u,
+                                                         double *__restrict__ sigma,
+                                                         int *__restrict__ info)
+{
+    extern __shared__ double jac_lds[];  // N columns of R (N = R rounded up to even)
+    __shared__ int rotated;
+    __shared__ double sg[128];
+    const int N = R + (R & 1);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = kJT / 64;
+    for (int e = threadIdx.x; e < N * R; e += kJT) {
+        const int j = e / R, i = e % R;
+        jac_lds[e] = j < R ? src[(size_t)j * lds + i] : 0.0;
+    }
+    const double tol = sqrt((double)R) * 0x1p-52;
+    int sweep = 0;
+    for (; sweep < kJacMaxSweeps; ++sweep) {
+        if (threadIdx.x == 0) rotated = 0;
+        __syncthreads();
+        for (int st = 0; st < N - 1; ++st) {
+            for (int pi = wv; pi < N / 2; pi += nw) {
+                const int kp = pi, kq = N - 1 - pi;
+                const int p = kp == 0 ? 0 : 1 + (kp - 1 + st) % (N - 1);
+                const int q = 1 + (kq - 1 + st) % (N - 1);
+                if (p >= R || q >= R) continue;  // the padding column
+                double *ap = jac_lds + (size_t)p * R, *aq = jac_lds + (size_t)q * R;
+                double x0 = lane < R ? ap[lane] : 0.0, y0 = lane < R ? aq[lane] : 0.0;
+                double x1 = lane + 64 < R ? ap[lane + 64] : 0.0;
+                double y1 = lane + 64 < R ? aq[lane + 64] : 0.0;
+                double a = x0 * x0 + x1 * x1, b = y0 * y0 + y1 * y1, g = x0 * y0 + x1 * y1;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    a += __shfl_xor(a, o);
+                    b += __shfl_xor(b, o);
+                    g += __shfl_xor(g, o);
+                }
+                if (!(fabs(g) > tol * sqrt(a * b))) continue;  // wave-uniform
+                const double z = (b - a) / (2.0 * g);
+                const double t = (z >= 0.0 ? 1.0 : -1.0) / (fabs(z) + sqrt(1.0 + z * z));
+                const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+                if (lane < R) {
+                    ap[lane] = c * x0 - s * y0;
+                    aq[lane] = s * x0 + c * y0;
+                }
+                if (lane + 64 < R) {
+                    ap[lane + 64] = c * x1 - s * y1;
+                    aq[lane + 64] = s * x1 + c * y1;
+                }
+                if (lane == 0) atomicAdd(&rotated, 1);
+            }
+            __syncthreads();
+        }
+        if (rotated == 0) break;
+        __syncthreads();  // everyone has read `rotated` before it is reset
+    }
+    // sigma_j = ||a_j||, ranks by decreasing sigma (ties by index)
+    for (int j = wv; j < R; j += nw) {
+        const double *aj = jac_lds + (size_t)j * R;
+        double x0 = lane < R ? aj[lane] : 0.0, x1 = lane + 64 < R ? aj[lane + 64] : 0.0;
+        double a = x0 * x0 + x1 * x1;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o);
+        if (lane == 0) sg[j] = sqrt(a);
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < R; j += kJT) {
+        int rank = 0;
+        for (int i = 0; i < R; ++i) rank += sg[i] > sg[j] || (sg[i] == sg[j] && i < j);
+        sigma[rank] = sg[j];
+        const double inv = sg[j] > 0.0 ? 1.0 / sg[j] : 0.0;
+        for (int i = 0; i < R; ++i) u[(size_t)rank * R + i] = jac_lds[(size_t)j * R + i] * inv;
+    }
+    if (threadIdx.x == 0) *info = sweep < kJacMaxSweeps ? 0 : 1;
+}
+
+size_t jacobi_lds_bytes(int R) { return sizeof(double) * (size_t)(R + (R & 1)) * R; }
+
+// out (K x n, row stride ldo) = sum over p < parts of W[p] (K x nc packed):
+// groups of parts summed into tmp[g] (gridDim.y = groups), then the groups --
+// a fixed order (deterministic), without one thread walking every part
+__global__ __launch_bounds__(kPB) void sum_rows_group_kernel(const double *__restrict__ w,
+                                                             int parts, int K, int nc, int n,
+                                                             double *__restrict__ tmp)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= (size_t)K * n) return;
+    const int G = gridDim.y, g = blockIdx.y;
+    const int p0 = (int)((long)parts * g / G), p1 = (int)((long)parts * (g + 1) / G);
+    const size_t j = e / n, c = e % n;
+    const size_t kn = (size_t)K * nc;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int p = p0;
+    for (; p + 3 < p1; p += 4) {
+        s0 += w[p * kn + j * nc + c];
+        s1 += w[(p + 1) * kn + j * nc + c];
+        s2 += w[(p + 2) * kn + j * nc + c];
+        s3 += w[(p + 3) * kn + j * nc + c];
+    }
+    for (; p < p1; ++p) s0 += w[p * kn + j * nc + c];
+    tmp[(size_t)g * K * n + e] = (s0 + s1) + (s2 + s3);
+}
+
+// C (m x n, ldc) = A (m x K, lda) B (K x n, ldb), all row-major, n <= 128
+int ts_gemm_nn(hipStream_t st, const double *a, size_t lda, size_t m, int K, const double *b,
+               size_t ldb, int n, double *c, size_t ldc)
+{
+    TsArgs g{a, b, c, lda, ldb, ldc, m, K, n, 0, 0};
+    const dim3 grid((unsigned)((m + 127) / 128));
+    switch ((n + 15) / 16) {
+    case 1: hipLaunchKernelGGL(gemm_nn_kernel<1>, grid, dim3(kTW), 0, st, g); break;
+    case 2: hipLaunchKernelGGL(gemm_nn_kernel<2>, grid, dim3(kTW), 0, st, g); break;
+    case 3: hipLaunchKernelGGL(gemm_nn_kernel<3>, grid, dim3(kTW), 0, st, g); break;
+    case 4: hipLaunchKernelGGL(gemm_nn_kernel<4>, grid, dim3(kTW), 0, st, g); break;
+    case 5: hipLaunchKernelGGL(gemm_nn_kernel<5>, grid, dim3(kTW), 0, st, g); break;
+    case 6: hipLaunchKernelGGL(gemm_nn_kernel<6>, grid, dim3(kTW), 0, st, g); break;
+    case 7: hipLaunchKernelGGL(gemm_nn_kernel<7>, grid, dim3(kTW), 0, st, g); break;
+    case 8: hipLaunchKernelGGL(gemm_nn_kernel<8>, grid, dim3(kTW), 0, st, g); break;
+    default: return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+// row parts of a tn product: a multiple of 8 (one set per XCD), >= ~8
+// workgroups per CU over the launch, >= 128 rows each, <= 512
+int ts_tn_parts(size_t m, int K)
+{
+    const int jt = (K + 127) / 128;
+    long p = 8L * ((2048 + 8L * jt - 1) / (8L * jt));
+    if (const char *e = std::getenv("BURG_POD_TN_PARTS")) p = std::max(8L, 8L * (std::atol(e) / 8));
+    while (p > 8 && (long)(m / (size_t)p) < 128) p -= 8;
+    return (int)std::min(p, 512L);
+}
+
+// groups of parts in the first reduction pass: ~16 parts each
+int ts_tn_groups(int parts) { return std::max(1, parts / 16); }
+
+// out (K x n, ldo) = A^T B for A (m x K, lda) and B (m x n, ldb) row-major,
+// n <= 128; work: ts_tn_work(m, K, n) doubles
+int ts_gemm_tn(hipStream_t st, const double *a, size_t lda, size_t m, int K, const double *b,
+               size_t ldb, int n, double *out, int ldo, double *work)
+{
+    const int NB = (n + 15) / 16;
+    if (NB < 1 || NB > 8) return -1;
+    const int parts = ts_tn_parts(m, K), jt = (K + 127) / 128;
+    TsArgs g{a, b, work, lda, ldb, 0, m, K, n, jt, (m + parts - 1) / parts};
+    const dim3 grid((unsigned)(parts * jt));
+    switch (NB) {
+    case 1: hipLaunchKernelGGL(gemm_tn_kernel<1>, grid, dim3(kTW), 0, st, g); break;
+    case 2: hipLaunchKernelGGL(gemm_tn_kernel<2>, grid, dim3(kTW), 0, st, g); break;
+    case 3: hipLaunchKernelGGL(gemm_tn_kernel<3>, grid, dim3(kTW), 0, st, g); break;
+    case 4: hipLaunchKernelGGL(gemm_tn_kernel<4>, grid, dim3(kTW), 0, st, g); break;
+    case 5: hipLaunchKernelGGL(gemm_tn_kernel<5>, grid, dim3(kTW), 0, st, g); break;
+    case 6: hipLaunchKernelGGL(gemm_tn_kernel<6>, grid, dim3(kTW), 0, st, g); break;
+    case 7: hipLaunchKernelGGL(gemm_tn_kernel<7>, grid, dim3(kTW), 0, st, g); break;
+    default: hipLaunchKernelGGL(gemm_tn_kernel<8>, grid, dim3(kTW), 0, st, g); break;
+    }
+    const int G = ts_tn_groups(parts);
+    double *tmp = work + (size_t)parts * K * 16 * NB;
+    hipLaunchKernelGGL(sum_rows_group_kernel, dim3(blocks((size_t)K * n), G), dim3(kPB), 0, st,
+                       (const double *)work, parts, K, 16 * NB, n, tmp);
+    hipLaunchKernelGGL(sum_rows_kernel, dim3(blocks((size_t)K * n)), dim3(kPB), 0, st,
+                       (const double *)tmp, G, K, n, n, out, ldo);
+    return hipGetLastError() == hipSuccess ? 0 : -3;
+}
+
+size_t ts_tn_work(size_t m, int K, int n)
+{
+    const int parts = ts_tn_parts(m, K);
+    return (size_t)parts * K * 16 * ((n + 15) / 16) + (size_t)ts_tn_groups(parts) * K * n;
+}
+
+// dst (rows x ldd, row-major, columns >= cols zero) <- src (rows x cols column-major, lds)
+__global__ __launch_bounds__(kPB) void cm_to_rm_pad_kernel(const double *__restrict__ src,
+                                                           size_t lds, size_t rows, int cols,
+                                                           double *__restrict__ dst, int ldd)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= rows * ldd) return;
+    const size_t r = e / ldd;
+    const int c = (int)(e % ldd);
+    dst[e] = c < cols ? src[(size_t)c * lds + r] : 0.0;
+}
+
+// svd_flip on a row-major (m x k) U: per column the sign of its first
+// largest-|.| entry; pass 1 per row chunk (thread = column), pass 2 over the
+// chunks in order, pass 3 scales.
+constexpr int kFlipRows = 1024;
+__global__ __launch_bounds__(128) void rm_colmax_kernel(const double *__restrict__ u, size_t m,
+                                                        int k, double *__restrict__ part)
+{
+    const int c = threadIdx.x;
+    if (c >= k) return;
+    const size_t r0 = (size_t)blockIdx.x * kFlipRows, r1 = std::min(m, r0 + kFlipRows);
+    double best = -1.0, val = 0.0;
+    for (size_t r = r0; r < r1; ++r) {
+        const double v = u[r * k + c];
+        if (fabs(v) > best) best = fabs(v), val = v;
+    }
+    part[((size_t)blockIdx.x * k + c) * 2] = best;
+    part[((size_t)blockIdx.x * k + c) * 2 + 1] = val;
+}
+
+__global__ __launch_bounds__(128) void rm_colsign_kernel(const double *__restrict__ part,
+                                                         int nparts, int k,
+                                                         double *__restrict__ sgn)
+{
+    const int c = threadIdx.x;
+    if (c >= k) return;
+    double best = -1.0, val = 0.0;
+    for (int p = 0; p < nparts; ++p) {
+        const double b = part[((size_t)p * k + c) * 2];
+        if (b > best) best = b, val = part[((size_t)p * k + c) * 2 + 1];
+    }
+    sgn[c] = val < 0.0 ? -1.0 : 1.0;
+}
+
+__global__ __launch_bounds__(kPB) void rm_colscale_kernel(double *__restrict__ u, size_t m, int k,
+                                                          const double *__restrict__ sgn)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= m * k) return;
+    u[e] *= sgn[e % k];
+}
+
+// U_B[:, :k] (R x R column-major, ld R) -> row-major (Rp x k), rows >= R zero
+__global__ __launch_bounds__(kPB) void ub_rows_kernel(const double *__restrict__ ub, int R, int k,
+                                                      int Rp, double *__restrict__ out)
+{
+    const size_t e = (size_t)blockIdx.x * kPB + threadIdx.x;
+    if (e >= (size_t)Rp * k) return;
+    const int r = (int)(e / k), c = (int)(e % k);
+    out[e] = r < R ? ub[(size_t)c * R + r] : 0.0;
+}
+
+// Orthonormal basis of the columns of a row-major Y (rows x R, row stride
+// Rp) in place: the shifted CholeskyQR3 of orth_columns with the Gram on
+// gemm_tn_kernel and Y <- Y R^-1 as the transposed left solve on the
+// column-major view Y^T (R x rows, ld Rp).  Householder fallback through a
+// column-major copy (tmp: rows x Rp, allocated on demand).
+rocblas_status orth_rows(rocblas_handle h, hipStream_t st, size_t rows, int R, int Rp, double *y,
+                         double *g, double *tau, rocblas_int *info, double *work, double **tmp,
+                         bool *householder)
+{
+    const double one = 1.0;
+    const double u = 0x1p-53;
+    const double c = 11.0 * ((double)rows * R + (double)R * (R + 1)) * u;
+    rocblas_status s;
+    *householder = false;
+    for (int pass = 0; pass < 3; ++pass) {
+        if (ts_gemm_tn(st, y, Rp, rows, Rp, y, Rp, Rp, g, Rp, work))
+            return rocblas_status_internal_error;
+        if (pass == 0)
+            hipLaunchKernelGGL(shift_diag_kernel, dim3(1), dim3(kPB), 0, st, g, R, c, Rp);
+        if ((s = rocsolver_dpotrf(h, rocblas_fill_upper, R, g, Rp, info)) != rocblas_status_success)
+            return s;
+        rocblas_int hinfo = 0;
+        if (hipMemcpyAsync(&hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return rocblas_status_internal_error;
+        if (hinfo != 0) {  // Y is left as the last successful pass made it: same span
+            *householder = true;
+            if (!*tmp && hipMalloc(tmp, sizeof(double) * rows * Rp) != hipSuccess)
+                return rocblas_status_memory_error;
+            // row-major (rows x Rp) -> column-major (rows x Rp), QR, and back
+            if (launch_basis_transpose(y, *tmp, rows, Rp, st)) return rocblas_status_internal_error;
+            if ((s = rocsolver_dgeqrf(h, (rocblas_int)rows, R, *tmp, (rocblas_int)rows, tau)) !=
+                    rocblas_status_success ||
+                (s = rocsolver_dorgqr(h, (rocblas_int)rows, R, R, *tmp, (rocblas_int)rows, tau)) !=
+                    rocblas_status_success)
+                return s;
+            if (launch_basis_transpose(*tmp, y, (size_t)Rp, (int)rows, st))
+                return rocblas_status_internal_error;
+            return rocblas_status_success;
+        }
+        if ((s = rocblas_dtrsm(h, rocblas_side_left, rocblas_fill_upper, rocblas_operation_transpose,
+                               rocblas_diagonal_non_unit, R, (rocblas_int)rows, &one, g, Rp, y,
+                               Rp)) != rocblas_status_success)
+            return s;
+    }
+    return rocblas_status_success;
+}
+
 }  // namespace
+
+int pod_rsvd_mfma(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
+                  int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,
+                  size_t msglen);
 
 int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, double *d_u,
                double *d_sigma, char *msg, size_t msglen)
@@ -321,6 +847,9 @@ int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, 
         snprintf(msg, msglen, "rsvd: need ns <= m < 2^31 and k <= nrand <= ns");
         return -1;
     }
+    const char *gemm = std::getenv("BURG_POD_GEMM");  // "rocblas": the library products below
+    if (nrand <= 128 && !(gemm && std::strcmp(gemm, "rocblas") == 0))
+        return pod_rsvd_mfma(st, m, ns, d_s, k, nrand, n_iter, d_omega, d_u, d_sigma, msg, msglen);
     const rocblas_int M = (rocblas_int)m, NS = ns, R = nrand;
     double *a = nullptr, *y = nullptr, *z = nullptr, *tau = nullptr, *b = nullptr, *ub = nullptr,
            *sv = nullptr, *e = nullptr, *c = nullptr, *sgn = nullptr, *g = nullptr,
@@ -409,6 +938,156 @@ int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, 
         cleanup();
         return err("transpose back", rc);
     }
+    (void)hipMemcpyAsync(d_sigma, sv, sizeof(double) * k, hipMemcpyDeviceToDevice, st);
+    rocblas_int hinfo = 0;
+    (void)hipMemcpyAsync(&hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return err("rsvd stream", 0);
+    }
+    cleanup();
+    if (hinfo != 0) {
+        snprintf(msg, msglen, "rocsolver_dgesvd did not converge (info=%d)", (int)hinfo);
+        return -6;
+    }
+    return 0;
+}
+
+// The randomized SVD of pod_rsvd_device on the tall-skinny MFMA products
+// (gemm_nn_kernel / gemm_tn_kernel): the same algorithm and the same
+// CholeskyQR3 normaliser, with S read in place (C-order, no transposed copy)
+// and every thin matrix row-major with Rp = 16 ceil(nrand / 16) columns (the
+// padding columns are zero throughout):
+//   Y = S Omega; n_iter x { Y = orth(Y); Z = orth(S^T Y); Y = S Z };
+//   Q = orth(Y); B^T = S^T Q (ns x Rp row-major = B, R x ns column-major,
+//   ld Rp); B = U_B Sigma V^T (rocSOLVER dgesvd); U = Q U_B[:, :k], written
+//   straight into the C-order (m x k) result.
+// nrand <= 128.
+int pod_rsvd_mfma(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
+                  int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,
+                  size_t msglen)
+{
+    auto err = [&](const char *what, int code) {
+        snprintf(msg, msglen, "%s failed (%d)", what, code);
+        return -3;
+    };
+    if (m < (size_t)ns || m > 0x7fffffffULL || nrand < k || nrand > ns || nrand > 128) {
+        snprintf(msg, msglen, "rsvd: need ns <= m < 2^31 and k <= nrand <= min(ns, 128)");
+        return -1;
+    }
+    const int R = nrand, Rp = 16 * ((R + 15) / 16);
+    const size_t nsz = (size_t)ns;
+    const size_t nflip = (m + kFlipRows - 1) / kFlipRows;
+    const size_t work_doubles =
+        std::max({ts_tn_work(m, ns, Rp), ts_tn_work(m, Rp, Rp), ts_tn_work(nsz, Rp, Rp),
+                  2 * nflip * (size_t)k});
+    double *y = nullptr, *z = nullptr, *om = nullptr, *tau = nullptr, *b = nullptr, *ub = nullptr,
+           *ubk = nullptr, *sv = nullptr, *e = nullptr, *sgn = nullptr, *g = nullptr,
+           *work = nullptr, *tmp = nullptr;
+    rocblas_int *info = nullptr;
+    rocblas_handle h = nullptr;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        if (h) rocblas_destroy_handle(h);
+        for (double *p : {y, z, om, tau, b, ub, ubk, sv, e, sgn, g, work, tmp})
+            if (p) (void)hipFree(p);
+        if (info) (void)hipFree(info);
+    };
+    if (hipMalloc(&y, sizeof(double) * m * Rp) != hipSuccess ||
+        hipMalloc(&z, sizeof(double) * nsz * Rp) != hipSuccess ||
+        hipMalloc(&om, sizeof(double) * nsz * Rp) != hipSuccess ||
+        hipMalloc(&tau, sizeof(double) * Rp) != hipSuccess ||
+        hipMalloc(&b, sizeof(double) * nsz * Rp) != hipSuccess ||
+        hipMalloc(&ub, sizeof(double) * (size_t)R * R) != hipSuccess ||
+        hipMalloc(&ubk, sizeof(double) * (size_t)Rp * k) != hipSuccess ||
+        hipMalloc(&sv, sizeof(double) * Rp) != hipSuccess ||
+        hipMalloc(&e, sizeof(double) * Rp) != hipSuccess ||
+        hipMalloc(&sgn, sizeof(double) * k) != hipSuccess ||
+        hipMalloc(&g, sizeof(double) * (size_t)Rp * Rp) != hipSuccess ||
+        hipMalloc(&work, sizeof(double) * work_doubles) != hipSuccess ||
+        hipMalloc(&info, sizeof(rocblas_int)) != hipSuccess) {
+        cleanup();
+        snprintf(msg, msglen, "rsvd: hipMalloc failed");
+        return -5;
+    }
+    if (rocblas_create_handle(&h) != rocblas_status_success) {
+        cleanup();
+        return err("rocblas_create_handle", 0);
+    }
+    rocblas_set_stream(h, st);
+    rocblas_status s;
+    bool hh = false;
+    int n_householder = 0;
+#define TS(call, what)                  \
+    if ((call) != 0) {                  \
+        cleanup();                      \
+        return err(what, 0);            \
+    }
+#define RS(call, what)                                \
+    if ((s = (call)) != rocblas_status_success) {     \
+        cleanup();                                    \
+        return err(what, (int)s);                     \
+    }
+    // Omega (ns x R column-major) -> row-major (ns x Rp)
+    hipLaunchKernelGGL(cm_to_rm_pad_kernel, dim3(blocks(nsz * Rp)), dim3(kPB), 0, st, d_omega, nsz,
+                       nsz, R, om, Rp);
+    TS(ts_gemm_nn(st, d_s, nsz, m, ns, om, Rp, Rp, y, Rp), "S.Omega");
+    for (int it = 0; it < n_iter; ++it) {
+        RS(orth_rows(h, st, m, R, Rp, y, g, tau, info, work, &tmp, &hh), "orth Y");
+        n_householder += hh;
+        TS(ts_gemm_tn(st, d_s, nsz, m, ns, y, Rp, Rp, z, Rp, work), "S^T.Q");
+        RS(orth_rows(h, st, nsz, R, Rp, z, g, tau, info, work, &tmp, &hh), "orth Z");
+        n_householder += hh;
+        TS(ts_gemm_nn(st, d_s, nsz, m, ns, z, Rp, Rp, y, Rp), "S.Z");
+    }
+    RS(orth_rows(h, st, m, R, Rp, y, g, tau, info, work, &tmp, &hh), "orth Q");
+    n_householder += hh;
+    if (std::getenv("BURG_POD_DEBUG"))
+        fprintf(stderr, "[pod] rsvd (mfma): %d of %d orthonormalisations fell back to Householder\n",
+                n_householder, 2 * n_iter + 1);
+    // B^T = S^T Q (ns x Rp row-major) = B (R x ns column-major, ld Rp)
+    TS(ts_gemm_tn(st, d_s, nsz, m, ns, y, Rp, Rp, b, Rp, work), "S^T.Q (B)");
+    const char *ssvd = std::getenv("BURG_POD_SMALL_SVD");  // "rocsolver": dgesvd of B itself
+    if (ssvd && std::strcmp(ssvd, "rocsolver") == 0) {
+        RS(rocsolver_dgesvd(h, rocblas_svect_singular, rocblas_svect_none, R, ns, b, Rp, sv, ub, R,
+                            nullptr, 1, e, rocblas_outofplace, info), "dgesvd B");
+    } else {
+        // B^T = Q_b R_b (CholeskyQR3 on a copy, R_b = Q_b^T B^T), so B = R_b^T Q_b^T and
+        // U_B, sigma are the left singular vectors and values of R_b^T (Jacobi, one workgroup)
+        if (hipMemcpyAsync(z, b, sizeof(double) * nsz * Rp, hipMemcpyDeviceToDevice, st) !=
+            hipSuccess) {
+            cleanup();
+            return err("copy B", 0);
+        }
+        RS(orth_rows(h, st, nsz, R, Rp, z, g, tau, info, work, &tmp, &hh), "orth B^T");
+        n_householder += hh;
+        TS(ts_gemm_tn(st, z, Rp, nsz, Rp, b, Rp, Rp, g, Rp, work), "Q_b^T.B^T");
+        static bool lds_set = false;
+        if (!lds_set) {
+            if (hipFuncSetAttribute((const void *)jacobi_svd_kernel,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)jacobi_lds_bytes(128)) != hipSuccess) {
+                cleanup();
+                return err("jacobi LDS", 0);
+            }
+            lds_set = true;
+        }
+        hipLaunchKernelGGL(jacobi_svd_kernel, dim3(1), dim3(kJT), jacobi_lds_bytes(R), st,
+                           (const double *)g, Rp, R, ub, sv, (int *)info);
+        TS(hipGetLastError() != hipSuccess, "jacobi svd");
+    }
+    // U = Q U_B[:, :k]: U_B (R x R column-major) -> row-major (Rp x k), rows >= R zero
+    hipLaunchKernelGGL(ub_rows_kernel, dim3(blocks((size_t)Rp * k)), dim3(kPB), 0, st,
+                       (const double *)ub, R, k, Rp, ubk);
+    TS(ts_gemm_nn(st, y, Rp, m, Rp, ubk, k, k, d_u, k), "Q.U_B");
+    hipLaunchKernelGGL(rm_colmax_kernel, dim3((unsigned)nflip), dim3(128), 0, st,
+                       (const double *)d_u, m, k, work);
+    hipLaunchKernelGGL(rm_colsign_kernel, dim3(1), dim3(128), 0, st, (const double *)work,
+                       (int)nflip, k, sgn);
+    hipLaunchKernelGGL(rm_colscale_kernel, dim3(blocks(m * k)), dim3(kPB), 0, st, d_u, m, k,
+                       (const double *)sgn);
+#undef TS
+#undef RS
     (void)hipMemcpyAsync(d_sigma, sv, sizeof(double) * k, hipMemcpyDeviceToDevice, st);
     rocblas_int hinfo = 0;
     (void)hipMemcpyAsync(&hinfo, info, sizeof hinfo, hipMemcpyDeviceToHost, st);

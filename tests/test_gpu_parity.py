@@ -979,6 +979,49 @@ def test_pod_tall_ragged_and_errors(gpu):
                       _lib.dptr(sv), None) == _lib.BURG_EINVAL
 
 
+@pytest.mark.parametrize("k,nrand", [(95, 105), (100, 128), (30, 40), (120, 129)])
+def test_pod_rsvd_mfma_products_vs_rocblas(gpu, monkeypatch, k, nrand):
+    """The randomized SVD on the tall-skinny MFMA products (default for
+    nrand <= 128: S used in place, thin matrices row-major) against the same
+    algorithm on rocBLAS dgemm (BURG_POD_GEMM=rocblas) and against numpy's
+    SVD, on sizes off every tile (m = 2*61^2 rows, ns = 301 columns, ranks
+    padded to 48 / 112 / 128; nrand = 129 takes the library path either
+    way).  Bars: singular values to 1e-11 relative between the two paths and
+    to 1e-9 of numpy's for the leading half of the modes; well-separated modes equal up
+    to 1e-9 in |cos|."""
+    from finitedifference_amd import _lib
+    rng = np.random.default_rng(5)
+    m, ns = 2 * 61 * 61, 301
+    decay = np.exp(-np.arange(160) / 12.0)
+    S = (rng.standard_normal((m, 160)) * decay) @ rng.standard_normal((160, ns))
+    S += 1e-9 * rng.standard_normal((m, ns))
+    S = np.ascontiguousarray(S)
+    # column-major (ns x nrand): its C-order transpose
+    omega = np.ascontiguousarray(np.random.default_rng(7).standard_normal((nrand, ns)))
+    L = _lib.load()
+
+    def run(path):
+        monkeypatch.setenv("BURG_POD_GEMM", path)
+        U = np.zeros((m, k))
+        sv = np.zeros(k)
+        rc = L.burg_pod_rsvd(0, m, ns, _lib.dptr(S), k, nrand, 4, _lib.dptr(omega), _lib.dptr(U),
+                             _lib.dptr(sv), None)
+        assert rc == 0, L.burg_last_error().decode()
+        return U, sv
+
+    um, sm = run("mfma")
+    ur, sr = run("rocblas")
+    assert np.allclose(sm, sr, rtol=1e-11, atol=0)
+    sn = np.linalg.svd(S, compute_uv=False)
+    lead = min(k // 2, 40)  # the rsvd approximation's own error grows toward mode k
+    assert np.allclose(sm[:lead], sn[:lead], rtol=1e-9, atol=0)
+    keep = _pod_mode_mask(sr, rel_floor=1e-8, rel_gap=1e-4)
+    assert keep.sum() >= min(k, 30)
+    assert np.all(np.abs(np.sum(um[:, keep] * ur[:, keep], axis=0)) > 1 - 1e-9)
+    assert np.max(np.abs(um[:, keep] - ur[:, keep])) < 1e-7  # same svd_flip signs
+    assert np.max(np.abs(um.T @ um - np.eye(k))) < 1e-12
+
+
 def test_lspg_solve_kernel_path(gpu, monkeypatch):
     """BURG_LSPG_SOLVE=kernel selects the one-workgroup Cholesky kernel instead
     of rocSOLVER potrf/potrs: same Gauss-Newton counts and trajectory (within
