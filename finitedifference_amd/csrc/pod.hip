@@ -246,19 +246,54 @@ struct TsArgs {
     size_t part_rows; // tn: rows per part
 };
 
-template <int NB>
+// LDS row stride of the staged thin operand: the rows the 4 k slots read in
+// one instruction must fall in different bank halves (gemm_nn: slots 2 rows
+// apart -> +8; gemm_tn: slots 8 rows apart -> +2)
+template <int NB, bool NN>
+constexpr int ts_ldb() { return 16 * NB + (NN ? 8 : 2); }
+
+// reduction row of k slot s4 in MFMA step s (0..7) of a chunk: gemm_tn
+// 8 s4 + s; gemm_nn 8 (s / 2) + 2 s4 + s % 2 (a lane's A operands are then
+// 16-B pairs, and the 4 slots of a row read 64 contiguous bytes per load)
+template <bool NN>
+__device__ __forceinline__ int ts_krow(int s4, int s)
+{
+    return NN ? 8 * (s >> 1) + 2 * s4 + (s & 1) : 8 * s4 + s;
+}
+
+template <int NB, bool NN, int OCC>
 __device__ __forceinline__ void ts_mfma_chunk(const double *bs, int cl, int s4,
                                               const double (&av)[2][8], dbl4 (&acc)[2][NB])
 {
-    constexpr int LDB = 16 * NB + 2;  // +2: the 4 k slots' rows start 8 rows = 16 banks apart
+    constexpr int LDB = ts_ldb<NB, NN>();
+    if constexpr (OCC == 2) {  // registers are scarce; the other workgroup covers the reads
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const double *brow = bs + ts_krow<NN>(s4, s) * LDB + cl;
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) {
+                const double bv = brow[16 * cb];
+                acc[0][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0][s], bv, acc[0][cb], 0, 0, 0);
+                acc[1][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1][s], bv, acc[1][cb], 0, 0, 0);
+            }
+        }
+        return;
+    }
+    // the B operands of step s + 1 are read from LDS while the MFMAs of step s run
+    double bv[2][NB];
+#pragma unroll
+    for (int cb = 0; cb < NB; ++cb) bv[0][cb] = bs[ts_krow<NN>(s4, 0) * LDB + cl + 16 * cb];
 #pragma unroll
     for (int s = 0; s < 8; ++s) {
-        const double *brow = bs + (8 * s4 + s) * LDB + cl;
+        if (s < 7) {
+            const double *brow = bs + ts_krow<NN>(s4, s + 1) * LDB + cl;
+#pragma unroll
+            for (int cb = 0; cb < NB; ++cb) bv[(s + 1) & 1][cb] = brow[16 * cb];
+        }
 #pragma unroll
         for (int cb = 0; cb < NB; ++cb) {
-            const double bv = brow[16 * cb];
-            acc[0][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0][s], bv, acc[0][cb], 0, 0, 0);
-            acc[1][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1][s], bv, acc[1][cb], 0, 0, 0);
+            acc[0][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[0][s], bv[s & 1][cb], acc[0][cb], 0, 0, 0);
+            acc[1][cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[1][s], bv[s & 1][cb], acc[1][cb], 0, 0, 0);
         }
     }
 }
@@ -279,10 +314,10 @@ __device__ __forceinline__ void ts_load_b(const TsArgs &g, size_t r0, size_t r_e
     }
 }
 
-template <int NB>
+template <int NB, bool NN>
 __device__ __forceinline__ void ts_store_b(double *bs, const double (&bn)[2 * NB])
 {
-    constexpr int NC = 16 * NB, LDB = NC + 2;
+    constexpr int NC = 16 * NB, LDB = ts_ldb<NB, NN>();
 #pragma unroll
     for (int q = 0; q < 2 * NB; ++q) {
         const int e = threadIdx.x + kTW * q;
@@ -290,10 +325,16 @@ __device__ __forceinline__ void ts_store_b(double *bs, const double (&bn)[2 * NB
     }
 }
 
-template <int NB>
-__global__ __launch_bounds__(kTW) void gemm_nn_kernel(TsArgs g)
+typedef double dbl2u __attribute__((ext_vector_type(2), aligned(8)));
+
+// OCC = 1: one workgroup per CU (208 VGPRs + 112 accumulator AGPRs), the
+// next chunk's A operands prefetched into registers; OCC = 2: two per CU (<=
+// 256 registers a wave), A loaded after the barrier -- the other
+// workgroup's MFMAs cover the wait
+template <int NB, int OCC>
+__global__ __launch_bounds__(kTW, OCC) void gemm_nn_kernel(TsArgs g)
 {
-    constexpr int LDB = 16 * NB + 2;
+    constexpr int LDB = ts_ldb<NB, true>();
     __shared__ double bs[2][kTK * LDB];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cl = lane & 15, s4 = lane >> 4;
@@ -311,29 +352,48 @@ __global__ __launch_bounds__(kTW) void gemm_nn_kernel(TsArgs g)
         for (int cb = 0; cb < NB; ++cb) acc[rb][cb] = dbl4{0.0, 0.0, 0.0, 0.0};
     const int nch = (g.K + kTK - 1) / kTK;
     double av[2][8], an[2][8], bn[2 * NB];
-    auto load_a = [&](int ch) {
-        const int k0 = ch * kTK + 8 * s4;
+    auto load_a = [&](int ch, double (&an)[2][8]) {
+        const int kb = ch * kTK + 2 * s4;  // + 8 q + e for the operand of step 2 q + e
+        if (ch * kTK + kTK <= g.K) {        // whole chunk: 16-B loads (rows are 8-B aligned)
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+            for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-            for (int s = 0; s < 8; ++s) an[rb][s] = k0 + s < g.K ? ap[rb][k0 + s] : 0.0;
+                for (int q = 0; q < 4; ++q) {
+                    const dbl2u v = *(const dbl2u *)(ap[rb] + kb + 8 * q);
+                    an[rb][2 * q] = v.x;
+                    an[rb][2 * q + 1] = v.y;
+                }
+        } else {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const int k = kb + 8 * (s >> 1) + (s & 1);
+                    an[rb][s] = k < g.K ? ap[rb][k] : 0.0;
+                }
+        }
     };
-    load_a(0);
+    if constexpr (OCC == 1) load_a(0, an);
     ts_load_b<NB>(g, 0, (size_t)g.K, bn);
-    ts_store_b<NB>(bs[0], bn);
+    ts_store_b<NB, true>(bs[0], bn);
     for (int ch = 0; ch < nch; ++ch) {
         __syncthreads();
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
         const bool more = ch + 1 < nch;
-        if (more) {
-            load_a(ch + 1);
-            ts_load_b<NB>(g, (size_t)(ch + 1) * kTK, (size_t)g.K, bn);
+        if constexpr (OCC == 1) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
+            if (more) load_a(ch + 1, an);
+        } else {
+            load_a(ch, av);
         }
-        ts_mfma_chunk<NB>(bs[ch & 1], cl, s4, av, acc);
-        if (more) ts_store_b<NB>(bs[(ch + 1) & 1], bn);
+        // OCC = 1: the next B chunk in flight during the MFMAs; OCC = 2: loaded after
+        // them (registers: bn is not live across the MFMA block)
+        if (OCC == 1 && more) ts_load_b<NB>(g, (size_t)(ch + 1) * kTK, (size_t)g.K, bn);
+        ts_mfma_chunk<NB, true, OCC>(bs[ch & 1], cl, s4, av, acc);
+        if (OCC == 2 && more) ts_load_b<NB>(g, (size_t)(ch + 1) * kTK, (size_t)g.K, bn);
+        if (more) ts_store_b<NB, true>(bs[(ch + 1) & 1], bn);
     }
     // D layout of the f64 MFMA: column lane & 15, row (lane >> 4) + 4 q
 #pragma unroll
@@ -348,10 +408,10 @@ __global__ __launch_bounds__(kTW) void gemm_nn_kernel(TsArgs g)
             }
 }
 
-template <int NB>
-__global__ __launch_bounds__(kTW) void gemm_tn_kernel(TsArgs g)
+template <int NB, int OCC>
+__global__ __launch_bounds__(kTW, OCC) void gemm_tn_kernel(TsArgs g)
 {
-    constexpr int NC = 16 * NB, LDB = NC + 2;
+    constexpr int NC = 16 * NB, LDB = ts_ldb<NB, false>();
     __shared__ double bs[2][kTK * LDB];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int cl = lane & 15, s4 = lane >> 4;
@@ -375,32 +435,39 @@ __global__ __launch_bounds__(kTW) void gemm_tn_kernel(TsArgs g)
         for (int cb = 0; cb < NB; ++cb) acc[rb][cb] = dbl4{0.0, 0.0, 0.0, 0.0};
     const int nch = (int)((i_end - i_beg + kTK - 1) / kTK);
     double av[2][8], an[2][8], bn[2 * NB];
-    auto load_a = [&](int ch) {
+    auto load_a = [&](int ch, double (&an)[2][8]) {
         const size_t i0 = i_beg + (size_t)ch * kTK + 8 * s4;
 #pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
+        for (int rb = 0; rb < 2; ++rb) {
+            const double *p = ap[rb] + i0 * g.lda;
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
-                an[rb][s] = (jok[rb] && i0 + s < i_end) ? ap[rb][(i0 + s) * g.lda] : 0.0;
+            for (int s = 0; s < 8; ++s, p += g.lda)
+                an[rb][s] = (jok[rb] && i0 + s < i_end) ? *p : 0.0;
+        }
     };
     if (nch > 0) {
-        load_a(0);
+        if constexpr (OCC == 1) load_a(0, an);
         ts_load_b<NB>(g, i_beg, i_end, bn);
-        ts_store_b<NB>(bs[0], bn);
+        ts_store_b<NB, false>(bs[0], bn);
     }
     for (int ch = 0; ch < nch; ++ch) {
         __syncthreads();
-#pragma unroll
-        for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-            for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
         const bool more = ch + 1 < nch;
-        if (more) {
-            load_a(ch + 1);
-            ts_load_b<NB>(g, i_beg + (size_t)(ch + 1) * kTK, i_end, bn);
+        if constexpr (OCC == 1) {
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) av[rb][s] = an[rb][s];
+            if (more) load_a(ch + 1, an);
+        } else {
+            load_a(ch, av);
         }
-        ts_mfma_chunk<NB>(bs[ch & 1], cl, s4, av, acc);
-        if (more) ts_store_b<NB>(bs[(ch + 1) & 1], bn);
+        // OCC = 1: the next B chunk in flight during the MFMAs; OCC = 2: loaded after
+        // them (registers: bn is not live across the MFMA block)
+        if (OCC == 1 && more) ts_load_b<NB>(g, i_beg + (size_t)(ch + 1) * kTK, i_end, bn);
+        ts_mfma_chunk<NB, false, OCC>(bs[ch & 1], cl, s4, av, acc);
+        if (OCC == 2 && more) ts_load_b<NB>(g, i_beg + (size_t)(ch + 1) * kTK, i_end, bn);
+        if (more) ts_store_b<NB, false>(bs[(ch + 1) & 1], bn);
     }
     double *wp = g.c + (size_t)p * g.K * NC;
 #pragma unroll
@@ -545,21 +612,41 @@ __global__ __launch_bounds__(kPB) void sum_rows_group_kernel(const double *__res
     tmp[(size_t)g * K * n + e] = (s0 + s1) + (s2 + s3);
 }
 
+// workgroups per CU of the tall-skinny products (BURG_POD_GEMM_OCC = 1 or 2)
+int ts_occ()
+{
+    static const int occ = [] {
+        const char *e = std::getenv("BURG_POD_GEMM_OCC");
+        return e && std::atoi(e) == 1 ? 1 : 2;
+    }();
+    return occ;
+}
+
+template <void (*K1)(TsArgs), void (*K2)(TsArgs)>
+void launch_ts(int occ, dim3 grid, hipStream_t st, const TsArgs &g)
+{
+    if (occ == 2)
+        hipLaunchKernelGGL(K2, grid, dim3(kTW), 0, st, g);
+    else
+        hipLaunchKernelGGL(K1, grid, dim3(kTW), 0, st, g);
+}
+
 // C (m x n, ldc) = A (m x K, lda) B (K x n, ldb), all row-major, n <= 128
 int ts_gemm_nn(hipStream_t st, const double *a, size_t lda, size_t m, int K, const double *b,
                size_t ldb, int n, double *c, size_t ldc)
 {
     TsArgs g{a, b, c, lda, ldb, ldc, m, K, n, 0, 0};
     const dim3 grid((unsigned)((m + 127) / 128));
+    const int occ = ts_occ();
     switch ((n + 15) / 16) {
-    case 1: hipLaunchKernelGGL(gemm_nn_kernel<1>, grid, dim3(kTW), 0, st, g); break;
-    case 2: hipLaunchKernelGGL(gemm_nn_kernel<2>, grid, dim3(kTW), 0, st, g); break;
-    case 3: hipLaunchKernelGGL(gemm_nn_kernel<3>, grid, dim3(kTW), 0, st, g); break;
-    case 4: hipLaunchKernelGGL(gemm_nn_kernel<4>, grid, dim3(kTW), 0, st, g); break;
-    case 5: hipLaunchKernelGGL(gemm_nn_kernel<5>, grid, dim3(kTW), 0, st, g); break;
-    case 6: hipLaunchKernelGGL(gemm_nn_kernel<6>, grid, dim3(kTW), 0, st, g); break;
-    case 7: hipLaunchKernelGGL(gemm_nn_kernel<7>, grid, dim3(kTW), 0, st, g); break;
-    case 8: hipLaunchKernelGGL(gemm_nn_kernel<8>, grid, dim3(kTW), 0, st, g); break;
+    case 1: launch_ts<gemm_nn_kernel<1, 1>, gemm_nn_kernel<1, 2>>(occ, grid, st, g); break;
+    case 2: launch_ts<gemm_nn_kernel<2, 1>, gemm_nn_kernel<2, 2>>(occ, grid, st, g); break;
+    case 3: launch_ts<gemm_nn_kernel<3, 1>, gemm_nn_kernel<3, 2>>(occ, grid, st, g); break;
+    case 4: launch_ts<gemm_nn_kernel<4, 1>, gemm_nn_kernel<4, 2>>(occ, grid, st, g); break;
+    case 5: launch_ts<gemm_nn_kernel<5, 1>, gemm_nn_kernel<5, 2>>(occ, grid, st, g); break;
+    case 6: launch_ts<gemm_nn_kernel<6, 1>, gemm_nn_kernel<6, 2>>(occ, grid, st, g); break;
+    case 7: launch_ts<gemm_nn_kernel<7, 1>, gemm_nn_kernel<7, 2>>(occ, grid, st, g); break;
+    case 8: launch_ts<gemm_nn_kernel<8, 1>, gemm_nn_kernel<8, 2>>(occ, grid, st, g); break;
     default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -3;
@@ -589,15 +676,16 @@ int ts_gemm_tn(hipStream_t st, const double *a, size_t lda, size_t m, int K, con
     const int parts = ts_tn_parts(m, K), jt = (K + 127) / 128;
     TsArgs g{a, b, work, lda, ldb, 0, m, K, n, jt, (m + parts - 1) / parts};
     const dim3 grid((unsigned)(parts * jt));
+    const int occ = ts_occ();
     switch (NB) {
-    case 1: hipLaunchKernelGGL(gemm_tn_kernel<1>, grid, dim3(kTW), 0, st, g); break;
-    case 2: hipLaunchKernelGGL(gemm_tn_kernel<2>, grid, dim3(kTW), 0, st, g); break;
-    case 3: hipLaunchKernelGGL(gemm_tn_kernel<3>, grid, dim3(kTW), 0, st, g); break;
-    case 4: hipLaunchKernelGGL(gemm_tn_kernel<4>, grid, dim3(kTW), 0, st, g); break;
-    case 5: hipLaunchKernelGGL(gemm_tn_kernel<5>, grid, dim3(kTW), 0, st, g); break;
-    case 6: hipLaunchKernelGGL(gemm_tn_kernel<6>, grid, dim3(kTW), 0, st, g); break;
-    case 7: hipLaunchKernelGGL(gemm_tn_kernel<7>, grid, dim3(kTW), 0, st, g); break;
-    default: hipLaunchKernelGGL(gemm_tn_kernel<8>, grid, dim3(kTW), 0, st, g); break;
+    case 1: launch_ts<gemm_tn_kernel<1, 1>, gemm_tn_kernel<1, 2>>(occ, grid, st, g); break;
+    case 2: launch_ts<gemm_tn_kernel<2, 1>, gemm_tn_kernel<2, 2>>(occ, grid, st, g); break;
+    case 3: launch_ts<gemm_tn_kernel<3, 1>, gemm_tn_kernel<3, 2>>(occ, grid, st, g); break;
+    case 4: launch_ts<gemm_tn_kernel<4, 1>, gemm_tn_kernel<4, 2>>(occ, grid, st, g); break;
+    case 5: launch_ts<gemm_tn_kernel<5, 1>, gemm_tn_kernel<5, 2>>(occ, grid, st, g); break;
+    case 6: launch_ts<gemm_tn_kernel<6, 1>, gemm_tn_kernel<6, 2>>(occ, grid, st, g); break;
+    case 7: launch_ts<gemm_tn_kernel<7, 1>, gemm_tn_kernel<7, 2>>(occ, grid, st, g); break;
+    default: launch_ts<gemm_tn_kernel<8, 1>, gemm_tn_kernel<8, 2>>(occ, grid, st, g); break;
     }
     const int G = ts_tn_groups(parts);
     double *tmp = work + (size_t)parts * K * 16 * NB;
