@@ -34,3 +34,15 @@ def gpu():
     from finitedifference_amd import _lib
     _lib.load()
     return _lib
+
+
+@pytest.fixture(autouse=True)
+def _gpu_device_sync_after(request):
+    """After every gpu-marked test: synchronise the device, so an asynchronous
+    GPU fault fails the test that caused it, not the next one."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()

@@ -874,8 +874,9 @@ def test_lspg_step_counts_and_rank_errors(gpu, orc):
     assert np.allclose(rels, orels, rtol=1e-6, atol=1e-12)
     with pytest.raises(_lib.BurgersError):
         ctx.lspg(np.ones(P.m), 1, np.zeros((P.m, 128)))
-    with pytest.raises(_lib.BurgersError):  # J basis rank-deficient: two equal columns
+    with pytest.raises(_lib.BurgersError) as ei:  # J basis rank-deficient: two equal columns
         ctx.lspg(np.ones(P.m), 1, np.hstack([B[:, :3], B[:, :1]]))
+    assert ei.value.code == _lib.BURG_ENOCONV, str(ei.value)
     sq = make_ctx(N, ny=N + 3)
     with pytest.raises(_lib.BurgersError):
         sq.lspg(np.ones(2 * N * (N + 3)), 1, np.ones((2 * N * (N + 3), 2)))
@@ -1025,7 +1026,8 @@ def test_pod_rsvd_mfma_products_vs_rocblas(gpu, monkeypatch, k, nrand):
 def test_lspg_solve_kernel_path(gpu, monkeypatch):
     """BURG_LSPG_SOLVE=kernel selects the one-workgroup Cholesky kernel instead
     of rocSOLVER potrf/potrs: same Gauss-Newton counts and trajectory (within
-    round-off) on the reference's n24 case, and the rank check still fires."""
+    round-off) on the reference's n24 case, and the rank check still fires
+    (BURG_ENOCONV, not a HIP error)."""
     from finitedifference_amd import _lib
     from finitedifference_amd import hypernet2D as H
     g = golden("ref_lspg.npz")
@@ -1040,9 +1042,10 @@ def test_lspg_solve_kernel_path(gpu, monkeypatch):
                                                      verbose=False)
     assert na == nb == int(g["n24_its"].sum())
     assert rel(b, a) <= 1e-13 and rel(b, g["n24_snaps"]) <= REF_TOL
-    with pytest.raises(_lib.BurgersError):
+    with pytest.raises(_lib.BurgersError) as ei:
         H.inviscid_burgers_implicit2D_LSPG(gx, gy, np.ones(2 * N * N), dt, 1, (m1, m2),
                                            np.hstack([B[:, :3], B[:, :1]]), verbose=False)
+    assert ei.value.code == _lib.BURG_ENOCONV, str(ei.value)  # the rank check, not a HIP error
 
 
 # ------------------------------------------------- drop-in host surface --
