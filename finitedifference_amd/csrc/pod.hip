@@ -615,11 +615,8 @@ __global__ __launch_bounds__(kPB) void sum_rows_group_kernel(const double *__res
 // workgroups per CU of the tall-skinny products (BURG_POD_GEMM_OCC = 1 or 2)
 int ts_occ()
 {
-    static const int occ = [] {
-        const char *e = std::getenv("BURG_POD_GEMM_OCC");
-        return e && std::atoi(e) == 1 ? 1 : 2;
-    }();
-    return occ;
+    const char *e = std::getenv("BURG_POD_GEMM_OCC");  // read per launch (tests switch it)
+    return e && std::atoi(e) == 1 ? 1 : 2;
 }
 
 template <void (*K1)(TsArgs), void (*K2)(TsArgs)>

@@ -980,14 +980,16 @@ def test_pod_tall_ragged_and_errors(gpu):
                       _lib.dptr(sv), None) == _lib.BURG_EINVAL
 
 
-@pytest.mark.parametrize("k,nrand", [(95, 105), (100, 128), (30, 40), (120, 129)])
-def test_pod_rsvd_mfma_products_vs_rocblas(gpu, monkeypatch, k, nrand):
+@pytest.mark.parametrize("k,nrand,occ", [(95, 105, 2), (95, 105, 1), (100, 128, 2), (30, 40, 2),
+                                         (120, 129, 2)])
+def test_pod_rsvd_mfma_products_vs_rocblas(gpu, monkeypatch, k, nrand, occ):
     """The randomized SVD on the tall-skinny MFMA products (default for
     nrand <= 128: S used in place, thin matrices row-major) against the same
     algorithm on rocBLAS dgemm (BURG_POD_GEMM=rocblas) and against numpy's
     SVD, on sizes off every tile (m = 2*61^2 rows, ns = 301 columns, ranks
     padded to 48 / 112 / 128; nrand = 129 takes the library path either
-    way).  Bars: singular values to 1e-11 relative between the two paths and
+    way; occ: BURG_POD_GEMM_OCC, one or two workgroups per CU).  Bars:
+    singular values to 1e-11 relative between the two paths and
     to 1e-9 of numpy's for the leading half of the modes; well-separated modes equal up
     to 1e-9 in |cos|."""
     from finitedifference_amd import _lib
@@ -1000,6 +1002,8 @@ def test_pod_rsvd_mfma_products_vs_rocblas(gpu, monkeypatch, k, nrand):
     # column-major (ns x nrand): its C-order transpose
     omega = np.ascontiguousarray(np.random.default_rng(7).standard_normal((nrand, ns)))
     L = _lib.load()
+
+    monkeypatch.setenv("BURG_POD_GEMM_OCC", str(occ))
 
     def run(path):
         monkeypatch.setenv("BURG_POD_GEMM", path)
