@@ -649,12 +649,14 @@ int ts_gemm_nn(hipStream_t st, const double *a, size_t lda, size_t m, int K, con
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
-// row parts of a tn product: a multiple of 8 (one set per XCD), >= ~8
-// workgroups per CU over the launch, >= 128 rows each, <= 512
+// row parts of a tn product: a multiple of 8 (one set per XCD), ~4 000
+// workgroups over the launch (~8 rounds at two per CU; at 250^2 x 9 mu: 112
+// parts -- 68.8 ms per POD against 71.8-73.7 with 64 and 71.9 with 56,
+// profiles/r04/pod/parts_ab.txt), >= 128 rows each, <= 512
 int ts_tn_parts(size_t m, int K)
 {
     const int jt = (K + 127) / 128;
-    long p = 8L * ((2048 + 8L * jt - 1) / (8L * jt));
+    long p = 8L * ((4032 + 8L * jt - 1) / (8L * jt));
     if (const char *e = std::getenv("BURG_POD_TN_PARTS")) p = std::max(8L, 8L * (std::atol(e) / 8));
     while (p > 8 && (long)(m / (size_t)p) < 128) p -= 8;
     return (int)std::min(p, 512L);
