@@ -336,7 +336,7 @@ def rom_pipeline(N=250, T=500, npod=95, rom_steps=20):
     del sn
     # warm-up on a slice: loads the rocBLAS / rocSOLVER code objects, which the
     # first call in a process otherwise pays inside its timed region
-    H.POD(np.ascontiguousarray(S[:, :64]), num_modes=8, method="rsvd", random_state=0)
+    H.POD(np.ascontiguousarray(S[:, :256]), num_modes=npod, method="rsvd", random_state=0)
     u, s, pod_ms = H.POD(S, num_modes=npod, method="rsvd", random_state=0, return_ms=True)
     del S
     # the same flow with the snapshot set left on the device (burg_sweep_device
