@@ -919,8 +919,10 @@ int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, doubl
 // Y = S Omega, n_iter power iterations Y <- orth(S orth(S^T Y)), Q = orth(Y),
 // B = Q^T S, B = U_B Sigma V^T, U = Q U_B[:, :k].  Orthonormalisation by
 // shifted CholeskyQR3 (orth_columns; Householder QR as its fallback;
-// sklearn's 'auto' normaliser is LU, which spans the same subspace).  Every
-// product is a rocBLAS dgemm on the device.
+// sklearn's 'auto' normaliser is LU, which spans the same subspace).
+// nrand <= 128 goes to pod_rsvd_mfma (our products, below); here, for wider
+// sketches or BURG_POD_GEMM=rocblas, every product is a rocBLAS dgemm and
+// the small SVD rocSOLVER's dgesvd.
 // omega: (ns x nrand) column-major (host), k <= nrand <= ns.
 int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
                     int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,

@@ -294,9 +294,11 @@ def POD(snaps, num_modes=None, method="svd", random_state=None, *, device=0, ret
                        randomized_svd algorithm (10 oversamples, n_iter 7 if
                        num_modes < 0.1 min(m, ns) else 4, Gaussian test matrix
                        drawn from check_random_state(random_state) exactly as
-                       sklearn draws it): burg_pod_rsvd, rocBLAS dgemm + QR on
-                       the device.  The power iterations are normalised by QR
-                       (sklearn's 'auto' uses LU: same subspace).
+                       sklearn draws it): burg_pod_rsvd, the products with S
+                       on fp64 MFMA kernels, CholeskyQR3 and a Jacobi small
+                       SVD on the device.  The power iterations are
+                       normalised by QR (sklearn's 'auto' uses LU: same
+                       subspace).
     Column signs follow sklearn's svd_flip rule on u (largest-magnitude entry
     positive); np.linalg.svd's are arbitrary."""
     if method not in ("svd", "rsvd"):

@@ -391,10 +391,12 @@ int burg_pod(int device, int64_t m, int ns, const double *snaps, int k, double *
 
 /* Randomized truncated SVD, the algorithm of sklearn's randomized_svd that
  * POD(method='rsvd') calls (C/hypernet2D.py:2688-2692): Y = S omega, n_iter
- * power iterations (Householder-QR normalised), Q = orth(Y), SVD of Q^T S.
+ * power iterations (CholeskyQR3-normalised), Q = orth(Y), SVD of Q^T S.
  * omega: (ns x nrand) COLUMN-major host matrix (the caller's Gaussian draw,
  * nrand = k + oversamples, k <= nrand <= ns); other arguments as burg_pod.
- * All products are rocBLAS dgemm on the device. */
+ * nrand <= 128: the products with S run on the library's fp64 MFMA kernels
+ * (S read in place) and the small SVD is a one-workgroup Jacobi; above, or
+ * with BURG_POD_GEMM=rocblas, rocBLAS dgemm and rocSOLVER dgesvd. */
 int burg_pod_rsvd(int device, int64_t m, int ns, const double *snaps, int k, int nrand, int n_iter,
                   const double *omega, double *U, double *sigma, double *ms);
 /* burg_pod_rsvd (omega != NULL) or burg_pod (omega == NULL) on a snapshot
