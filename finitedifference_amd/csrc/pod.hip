@@ -546,6 +546,9 @@ __global__ __launch_bounds__(kJT) void jacobi_svd_kernel(const double *__restric
                     b += __shfl_xor(b, o);
                     g += __shfl_xor(g, o);
                 }
+                // the butterfly's lanes may differ in the last bit: take lane 0's
+                // sums, so every lane takes the same decision and the same angle
+                a = __shfl(a, 0), b = __shfl(b, 0), g = __shfl(g, 0);
                 if (!(fabs(g) > tol * sqrt(a * b))) continue;  // wave-uniform
                 const double z = (b - a) / (2.0 * g);
                 const double t = (z >= 0.0 ? 1.0 : -1.0) / (fabs(z) + sqrt(1.0 + z * z));
