@@ -3,7 +3,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-O=$GRAFT_REPO_ROOT/gpurun_out/r4z
+O=$GRAFT_REPO_ROOT/gpurun_out/r4z2
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "pod" > $O/pytest_pod.log 2>&1 || { tail -40 $O/pytest_pod.log; exit 1; }
 tail -2 $O/pytest_pod.log
