@@ -175,8 +175,12 @@ template <int W>
 constexpr int win_of() { return two_per_cu<W>() ? 12 : u16_of<W>() ? 32 : W >= 1024 ? 16 : BURG_KWIN; }  // window (diagonals)
 template <int W>
 constexpr int uw_of() { return two_per_cu<W>() ? 4 : u16_of<W>() ? 16 : 8; }  // block (diagonals)
+// (blocks of 16: 32 diagonals; BURG_U16_LA for A/B builds)
+#ifndef BURG_U16_LA
+#define BURG_U16_LA 32
+#endif
 template <int W>
-constexpr int la_of() { return u16_of<W>() ? 32 : BURG_KLA; }
+constexpr int la_of() { return u16_of<W>() ? BURG_U16_LA : BURG_KLA; }
 // LDS ring slots (steps) of the intra-workgroup west -> east edges
 template <int W>
 constexpr int rl_of() { return (u16_of<W>() || (W <= 16 && BURG_NARROW_U >= 16)) ? 2 : kPipeRL; }
