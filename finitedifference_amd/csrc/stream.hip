@@ -421,18 +421,21 @@ __device__ __forceinline__ long long ring_entry(const StreamArgs &a, int W, int 
 
 // C-order state w (u plane | v plane) -> ring entries of state 0.
 // Padding cells (rows >= ny, columns >= nx) get u = v = 1.  Consecutive
-// threads take consecutive columns of one row (coalesced reads of w; the
-// 16-B ring stores of a wave go to consecutive entries, and the other rows'
-// stores complete their lines in L2 soon after): 4096^2 249 us per load,
-// against 289 us with consecutive rows (8 B per row read), profiles/r04/ringload.
+// threads fill consecutive lanes of ONE ring entry (a skewed diagonal s =
+// cl + lane of the tile: 1 KB stores per wave) and read the state along that
+// diagonal (8 B per row; reads scattered rather than stores, as in
+// ring_extract_kernel): 4096^2 218 us per load, against 289 us with
+// consecutive lanes of one column (stores and reads scattered) and 249 us
+// with consecutive columns of one row (profiles/r04/ringload).
 __global__ void ring_load_kernel(StreamArgs a, int W, const double *w)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const size_t per_tile = (size_t)kWave * W;
+    const size_t per_tile = (size_t)kWave * (W + kWave - 1);
     if (i >= (size_t)a.ntiles * per_tile) return;
     const int tile = (int)(i / per_tile);
     const int rem = (int)(i - (size_t)tile * per_tile);
-    const int lane = rem / W, cl = rem % W;
+    const int lane = rem % kWave, cl = rem / kWave - lane;  // diagonal rem / kWave = cl + lane
+    if (cl < 0 || cl >= W) return;
     const int ti = tile / a.ntj, tj = tile % a.ntj;
     const int row = ti * kWave + lane, col = tj * W + cl;
     const size_t n = (size_t)a.cf.nx * a.cf.ny;
@@ -599,7 +602,7 @@ int launch_fill_sentinel(void *p, size_t n16, hipStream_t st)
 
 int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st)
 {
-    const size_t total = (size_t)a.ntiles * kWave * W;
+    const size_t total = (size_t)a.ntiles * kWave * (W + kWave - 1);
     hipLaunchKernelGGL(ring_load_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
                        a, W, w);
     return hipGetLastError() == hipSuccess ? 0 : -3;
