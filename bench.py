@@ -401,6 +401,16 @@ def read_clock(path, key):
     return e.get("effective_clock_ghz"), e.get("clock_source")
 
 
+def _lib_build_id():
+    from finitedifference_amd import _lib
+    return _lib.build_id()
+
+
+def _lib_source_id():
+    from finitedifference_amd import _lib
+    return _lib.source_id()
+
+
 def main():
     args = parse()
     rank, world, local = dist_env()
@@ -439,6 +449,13 @@ def main():
         c.set_problem(gx, gy, dt, MU, allow_nonsquare=(nx != ny))
         c.upload(np.ones(c.m))
         if nmu == 1:
+            if world > 1 and args.snap_every <= 0:
+                # "auto" resolves per rank from its own free HBM: agree on the
+                # largest stride, so every rank keeps the same states
+                k, _, _ = c.trajectory_plan(T, args.snap_every)
+                t = torch.tensor([k], dtype=torch.int64, device="cpu" if rehearse else "cuda")
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                args.snap_every = int(t.item())
             # the trajectory ring (134 GB at 4096^2 x 500 steps) is allocated
             # here, before the barrier: no rank's first launch waits on a
             # neighbour still allocating (the halo waits are bounded in time)
@@ -596,6 +613,7 @@ def main():
                 "halo_fallback": halo_fallback,
             },
             "residual_check": check,
+            "build_id": {"library": _lib_build_id(), "sources": _lib_source_id()},
             "engine": {"name": eng, "tile_w": st["stream_w"], "tiles": st["stream_tiles"],
                        "blocked_diagonals": st["slow_diagonals"],
                        "spin_polls": st["stall_spins"], "ieee_diagonals": st["ieee_diagonals"],

@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -30,7 +30,7 @@ EXPORTS = (
     "burg_trajectory_plan", "burg_trajectory_retained", "burg_trajectory_copy",
     "burg_sweep_device", "burg_pod_rsvd_device",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
-    "burg_pod", "burg_pod_rsvd", "burg_run_npy",
+    "burg_pod", "burg_pod_rsvd", "burg_run_npy", "burg_build_id", "burg_ring_audit",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -109,6 +109,8 @@ def load(path=None):
         sig = {
             "burg_abi_version": (ctypes.c_int, []),
             "burg_last_error": (ctypes.c_char_p, []),
+            "burg_build_id": (ctypes.c_char_p, []),
+            "burg_ring_audit": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_int64)]),
             "burg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.POINTER(_VP)]),
             "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.c_char_p,
@@ -187,6 +189,41 @@ def load(path=None):
             raise RuntimeError(f"{p}: ABI version {v}, expected {ABI_VERSION}")
         _lib = lib
         return lib
+
+
+_CSRC = os.path.join(_HERE, "csrc")
+
+
+def source_id(csrc=_CSRC):
+    """The digest burg_build_id() reports, computed from the sources in this
+    checkout (csrc/*.h and *.hip in byte order, then csrc/Makefile and
+    include/burgers.h -- the Makefile's BUILD_ID_SRCS)."""
+    import glob
+    import hashlib
+    names = sorted(os.path.basename(f) for f in glob.glob(os.path.join(csrc, "*.hip")) +
+                   glob.glob(os.path.join(csrc, "*.h")))
+    files = [os.path.join(csrc, n) for n in names]
+    files += [os.path.join(csrc, "Makefile"),
+              os.path.join(os.path.dirname(_HERE), "include", "burgers.h")]
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id():
+    """burg_build_id() of the loaded library."""
+    return load().burg_build_id().decode()
+
+
+def ring_audit(W, num_steps, snap_every=1, ring_cap=0):
+    """burg_ring_audit as a dict (host-only; no GPU needed)."""
+    rep = (ctypes.c_int64 * 9)()
+    check(load().burg_ring_audit(int(W), int(num_steps), int(snap_every), int(ring_cap), rep))
+    keys = ("accesses", "max_entry", "entries_per_tile", "out_of_range", "walk_mismatch",
+            "retained_overwritten", "early_overwrite", "retained_states", "snap_every")
+    return dict(zip(keys, list(rep)))
 
 
 def check(code, allow=()):

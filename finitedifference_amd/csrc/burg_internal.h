@@ -123,6 +123,39 @@ __host__ __device__ inline long long ring_pos(long long s, long long origin, lon
     return d < 0 ? d + L : d;
 }
 
+// Walk of a tile's diagonals one block of U at a time through the retained
+// windows of ring_pos (a.ret_k > 0): entry of the block's first diagonal,
+// advanced per block without divisions.  The windows, the working ring's
+// wrap (L a multiple of U, origin 0) and the blocks all start on multiples of
+// U, so a block's U diagonals are U consecutive entries.  s0: first diagonal
+// of the walk, <= 0.  A: any struct with origin, L, ret_k, ret_n, ret_base
+// (PipeArgs on the device; burg_ring_audit replays the same walk on the host).
+struct RetCursor {
+    int j, o;    // window index, diagonal - (window j's first diagonal)
+    unsigned w;  // working-ring position of the next diagonal outside a window
+    template <class A>
+    __host__ __device__ void init(const A &a, int W, int s0)
+    {
+        j = 0;
+        o = s0 - (a.ret_k - 1) * W;
+        long long e = (a.origin + s0) % a.L;
+        w = (unsigned)(e < 0 ? e + a.L : e);
+    }
+    template <class A>
+    __host__ __device__ unsigned next(const A &a, int W, int U)
+    {
+        const bool inw = (o >= 0) & (o < W + 64) & (j < a.ret_n);
+        const unsigned e = inw ? (unsigned)a.ret_base + (unsigned)(j * (W + 64) + o) : w;
+        if (!inw) w = w + U >= (unsigned)a.L ? w + U - (unsigned)a.L : w + U;
+        o += U;
+        if (o == a.ret_k * W) {
+            o = 0;
+            ++j;
+        }
+        return e;
+    }
+};
+
 struct StreamArgs {
     Coeffs cf;
     const d2 *colc;      // [ntj*W] {hx, src} per column
@@ -221,11 +254,14 @@ int launch_colc_batch(const Coeffs &cf, int nb, const double *src_b, int ncols_p
                       hipStream_t st);
 int launch_fill_sentinel(void *p, size_t n16, hipStream_t st);
 int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st);
+// (out_elems: doubles the caller's `out` holds -- the kernels check every
+// ring entry and output index, StreamArgs::err[5] flags a violation)
 int launch_ring_extract_rows(const StreamArgs &a, int W, size_t e0, size_t ne, int k0, int kstep,
-                             int ncols, double *out, hipStream_t st);
+                             int ncols, double *out, size_t out_elems, hipStream_t st);
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
-                        int ldo, hipStream_t st);
+                        int ldo, size_t out_elems, hipStream_t st);
 bool pipe_width_supported(int W);
+int pipe_block_of(int W);  // diagonals per block of the trajectory kernel
 bool pipe_sweep_width_supported(int W);
 int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
@@ -275,7 +311,19 @@ int pod_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, doubl
 int pod_rsvd_device(hipStream_t st, size_t m, int ns, const double *d_s, int k, int nrand,
                     int n_iter, const double *d_omega, double *d_u, double *d_sigma, char *msg,
                     size_t msglen);
+// (out_elems: doubles `out` holds; a write past it is dropped and sets *flag |= 2)
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
-                     int ldo, hipStream_t st);
+                     int ldo, size_t out_elems, unsigned *flag, hipStream_t st);
+
+// Copies between caller host memory and the device, through the library's
+// pinned bounce buffers (hostxfer.hip; synchronous: the caller's buffer is
+// free / filled on return).  No caller memory is ever handed to the HIP
+// runtime's copy engine or to hipHostRegister.
+hipError_t h2d(void *dst, const void *src, size_t bytes, hipStream_t st);
+hipError_t d2h(void *dst, const void *src, size_t bytes, hipStream_t st);
+hipError_t d2h_2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                  size_t height, hipStream_t st);
+hipError_t h2d_2d(void *dst, size_t dpitch, const void *src, size_t spitch, size_t width,
+                  size_t height, hipStream_t st);
 
 }  // namespace burg

@@ -6,6 +6,7 @@
 #include <rocblas/rocblas.h>
 
 #include <algorithm>
+#include <climits>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -24,6 +25,7 @@
 
 #include "../../include/burgers.h"
 #include "burg_internal.h"
+#include "build/build_id.h"
 
 using namespace burg;
 
@@ -378,6 +380,28 @@ void stream_free(burg_ctx *c)
     c->ring_entries = 0;
     c->ring_maxed = false;
     c->sp_ready = c->colc_ready = false;
+    c->tr.valid = false;  // the ring it described is gone
+}
+
+// err[5] of the context: the flat-pointer ring / transpose kernels' bounds
+// flag (stream.hip ring_ok / out_ok, stencil.hip transpose_kernel)
+unsigned *bflag(burg_ctx *c) { return c->d_err ? c->d_err + 5 : nullptr; }
+
+// after a copy: did a bounds guard fire?  (the stream is synchronised)
+int check_bounds(burg_ctx *c, const char *where)
+{
+    if (!c->d_err) return 0;
+    unsigned f = 0;
+    HIPCHK(hipMemcpyAsync(&f, c->d_err + 5, sizeof f, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!f) return 0;
+    (void)hipMemsetAsync(c->d_err + 5, 0, sizeof f, c->stream);
+    (void)hipStreamSynchronize(c->stream);
+    return fail(BURG_EHIP, "%s: internal bounds check failed (%s%s): a library bug -- please "
+                "report the grid, tile width and snap_every", where,
+                (f & 1) ? "ring entry outside the tile's ring" : "",
+                (f & 2) ? ((f & 1) ? ", output index past the buffer" : "output index past the buffer")
+                        : "");
 }
 
 // Pipe engine plan: the narrowest W in {8, 16, ..., 1024} whose tile count
@@ -444,7 +468,7 @@ int stream_setup(burg_ctx *c)
             if (int e = dalloc(&c->d_err, 8)) return e;
             if (int e = dalloc(&c->d_sstats, 1)) return e;
             CHK(launch_pipe_fill(c->d_boxes, c->box16, 0, c->stream));
-            HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_err, 0, 8 * sizeof(unsigned), c->stream));
             c->qbase = 0;
             c->sp_ready = true;
             c->colc_ready = false;
@@ -480,7 +504,7 @@ int stream_setup(burg_ctx *c)
             if (int e = dalloc(&c->d_err, 8)) return e;
             if (int e = dalloc(&c->d_sstats, 1)) return e;
             CHK(launch_fill_sentinel(c->d_boxes, c->box16, c->stream));
-            HIPCHK(hipMemsetAsync(c->d_err, 0, 4 * sizeof(unsigned), c->stream));
+            HIPCHK(hipMemsetAsync(c->d_err, 0, 8 * sizeof(unsigned), c->stream));
             c->sp_ready = true;
             c->colc_ready = false;
         }
@@ -775,9 +799,10 @@ int stream_advance(burg_ctx *c, int num_steps, burg_stats *st)
         // the final state is state `last` of the last launch (origin before it)
         const long long o_last = ((origin - (long long)last * W) % L + L) % L;
         CHK(launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1,
-                                c->d_state[c->cur ^ 1], 1, c->stream));
+                                c->d_state[c->cur ^ 1], 1, c->m(), c->stream));
         c->cur ^= 1;
     }
+    if (int e = check_bounds(c, "stream_advance")) return e;
     if (int e = stream_stats_end(c, st, num_steps, launches)) return e;
     if (st) {
         st->loop_ms = ms;
@@ -872,6 +897,31 @@ int resolve_snap_every(burg_ctx *c, int num_steps, int snap_every)
     return plain_ring_fits(c, num_steps) ? 1 : 10;
 }
 
+// The layout of a retained-window trajectory ring (pure arithmetic:
+// trajectory_ring and burg_ring_audit): a working ring of Lw entries -- up to
+// the whole trajectory's diagonals, at most Lw_cap (the memory budget), at
+// least 2W + 128, a multiple of every block length -- then n = num_steps / k
+// windows of W + 64 entries from entry Lw.  BURG_RET_LW=m: exactly m W + 128
+// (A/B knob).  False when even the shortest working ring does not fit.
+bool retained_layout(int W, int num_steps, int k, long long Lw_cap, TrajMap *mp)
+{
+    const int n = num_steps / k;
+    const long long Lwin = (long long)n * (W + 64);
+    long long Lw = (long long)num_steps * W + W + 96;
+    Lw = std::min(Lw, Lw_cap);
+    Lw = std::min(Lw, (1LL << 21) - 2 - Lwin);
+    Lw = Lw / 16 * 16;
+    if (const char *e = std::getenv("BURG_RET_LW")) Lw = std::max(2LL, std::atoll(e)) * W + 128;
+    *mp = TrajMap{};
+    mp->L = Lw;
+    mp->origin = 0;
+    mp->Lt = ring_stride(Lw + Lwin);
+    mp->base = Lw;
+    mp->k = k;
+    mp->n = n;
+    return Lw >= 2LL * W + 128;
+}
+
 // The ring of a trajectory keeping every snap_every-th state (DESIGN.md
 // section 4.1d).  snap_every = 1: the plain ring (every state while it fits;
 // capped by free HBM it keeps the last C).  snap_every = k >= 2 on the pipe
@@ -904,22 +954,16 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
         // ring of 2W + 128 entries the windowed trajectory ran 93-95 ms on
         // some boxes and allocations and 110-112 ms on others, while the
         // plain capped ring held 93-95 ms everywhere, profiles/r04/
-        // ret_variance.)  At least 2W + 128 entries, a multiple of every block
-        // length.  BURG_RET_LW=m: exactly m W + 128 (A/B knob).
-        long long Lw = (long long)num_steps * W + W + 96;
+        // ret_variance.)
         const long long Lmem = avail > ret0 ? (long long)((avail - ret0) / per_entry) - Lwin - 2 : 0;
-        Lw = std::min(Lw, Lmem);
-        Lw = std::min(Lw, (1LL << 21) - 2 - Lwin);
-        Lw = Lw / 16 * 16;
-        if (const char *e = std::getenv("BURG_RET_LW")) Lw = std::max(2LL, std::atoll(e)) * W + 128;
-        if (Lw < 2LL * W + 128) {
+        if (!retained_layout(W, num_steps, k, Lmem, mp)) {
             if (Lwin + 2LL * W + 128 >= (1LL << 21))
                 return fail(BURG_ESHAPE, "%d retained states of %d-wide tiles exceed one buffer "
                             "descriptor per tile (2 GiB); raise snap_every", n, W);
             return fail(BURG_ENOMEM, "%d retained states (%.1f GB) do not fit in HBM; raise "
                         "snap_every", n, (double)(Lwin + 2LL * W + 128) * per_entry / 1e9);
         }
-        const long long Lt = ring_stride(Lw + Lwin);
+        const long long Lt = mp->Lt;
         const size_t need = (size_t)Lt * per_entry;
         if (need > have || have > need + need / 4 + ((size_t)1 << 30)) {
             dfree(c->d_ring);
@@ -928,12 +972,6 @@ int trajectory_ring(burg_ctx *c, int num_steps, int snap_every, TrajMap *mp, lon
         if (int e = ensure_ring(c, Lt)) return e;
         if (!c->d_ret0)
             if (int e = dalloc(&c->d_ret0, c->m())) return e;
-        mp->L = Lw;
-        mp->origin = 0;
-        mp->Lt = Lt;
-        mp->base = Lw;
-        mp->k = k;
-        mp->n = n;
         *C_out = num_steps;
         return 0;
     }
@@ -1006,7 +1044,8 @@ int stream_trajectory(burg_ctx *c, int num_steps, int snap_every, bool from_init
     const long long o_last = ((origin - (long long)last * W) % mp.L + mp.L) % mp.L;
     mp.origin = o_last;
     CHK(launch_ring_extract(stream_args(c, mp.L, o_last, 0, &mp), W, last, 1, 1,
-                            c->d_state[c->cur ^ 1], 1, c->stream));
+                            c->d_state[c->cur ^ 1], 1, c->m(), c->stream));
+    if (int e = check_bounds(c, "trajectory")) return e;
     c->cur ^= 1;
     // what stays resident
     TrajRecord &tr = c->tr;
@@ -1076,16 +1115,12 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
     // snapshot staging: S columns at a time
     int S = 0;
     double *d_tr = nullptr;
-    bool registered = false;
     const int64_t ncols = num_steps / snap_every + 1;
     if (snaps) {
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
         S = (int)std::min<int64_t>(ncols, 64);
         while (S > 1 && (size_t)S * bytes > freeb / 3) S /= 2;
         if (int e = dalloc(&d_tr, (size_t)S * m)) return e;
-        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
-                                     hipHostRegisterDefault) == hipSuccess;
-        (void)hipGetLastError();
     }
     float flush_ms = 0.f;
     hipEvent_t f0 = nullptr, f1 = nullptr;
@@ -1097,10 +1132,9 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
             const int n = std::min(S, cnt - j0);
             HIPCHK(hipEventRecord(f0, c->stream));
             CHK(launch_ring_extract(stream_args(c, L, origin, 0), W, k0 + j0 * snap_every,
-                                    snap_every, n, d_tr, n, c->stream));
-            HIPCHK(hipMemcpy2DAsync(snaps + col + j0, (size_t)ld_snaps * sizeof(double), d_tr,
-                                    n * sizeof(double), n * sizeof(double), m,
-                                    hipMemcpyDeviceToHost, c->stream));
+                                    snap_every, n, d_tr, n, (size_t)S * m, c->stream));
+            HIPCHK(d2h_2d(snaps + col + j0, (size_t)ld_snaps * sizeof(double), d_tr,
+                          n * sizeof(double), n * sizeof(double), m, c->stream));
             HIPCHK(hipEventRecord(f1, c->stream));
             HIPCHK(hipEventSynchronize(f1));
             float t = 0.f;
@@ -1112,7 +1146,7 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
 
     int rc = BURG_OK;
     stream_stats_begin(c);
-    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_state[c->cur], w0, bytes, c->stream));
     CHK(launch_ring_load(stream_args(c, L, 0, 0), W, c->d_state[c->cur], c->stream));
     if (snaps) rc = flush(0, 0, 1, 0);
     float ms = 0.f;
@@ -1137,10 +1171,11 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
     if (rc == BURG_OK && num_steps > 0) {
         const long long o_last = ((origin - (long long)last * W) % L + L) % L;
         rc = launch_ring_extract(stream_args(c, L, o_last, 0), W, last, 1, 1,
-                                 c->d_state[c->cur ^ 1], 1, c->stream);
+                                 c->d_state[c->cur ^ 1], 1, m, c->stream);
         if (rc == -3) rc = fail(BURG_EHIP, "ring extract launch failed");
         else c->cur ^= 1;
     }
+    if (rc == BURG_OK) rc = check_bounds(c, "burg_run (stream)");
     if (rc == BURG_OK) rc = stream_stats_end(c, st, num_steps, launches);
     if (st) {
         st->loop_ms = ms;
@@ -1155,7 +1190,6 @@ int stream_run(burg_ctx *c, const double *w0, int num_steps, double *snaps, int6
         if (step_rel) step_rel[s] = 0.0;
     }
     (void)hipStreamSynchronize(c->stream);
-    if (registered) (void)hipHostUnregister(snaps);
     dfree(d_tr);
     // the ring of a long run can be large: give it back
     dfree(c->d_ring);
@@ -1558,14 +1592,10 @@ int burg_set_problem(burg_ctx *c, const double *inv_dx, const double *inv_dy,
         if (int e = dalloc(&c->d_src, (size_t)c->nx)) return e;
         if (int e = dalloc(&c->d_lbc, (size_t)c->ny_total)) return e;
     }
-    HIPCHK(hipMemcpyAsync(c->d_inv_dx, inv_dx, sizeof(double) * c->nx, hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_inv_dy, inv_dy, sizeof(double) * c->ny_total,
-                          hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_src, src, sizeof(double) * c->nx, hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_lbc, lbc, sizeof(double) * c->ny_total, hipMemcpyHostToDevice,
-                          c->stream));
+    HIPCHK(h2d(c->d_inv_dx, inv_dx, sizeof(double) * c->nx, c->stream));
+    HIPCHK(h2d(c->d_inv_dy, inv_dy, sizeof(double) * c->ny_total, c->stream));
+    HIPCHK(h2d(c->d_src, src, sizeof(double) * c->nx, c->stream));
+    HIPCHK(h2d(c->d_lbc, lbc, sizeof(double) * c->ny_total, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->dt = dt;
     c->cf.inv_dx = c->d_inv_dx;
@@ -1623,11 +1653,11 @@ int burg_residual(burg_ctx *c, const double *w, const double *wp, double *r, dou
     if (!w || !wp || !r) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
     const size_t bytes = c->m() * sizeof(double);
-    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_d, wp, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_x, w, bytes, c->stream));
+    HIPCHK(h2d(c->d_d, wp, bytes, c->stream));
     double nrm = 0.0;
     if (int e = residual_norm(c, c->d_x, c->d_d, c->d_r, &nrm)) return e;
-    HIPCHK(hipMemcpyAsync(r, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(d2h(r, c->d_r, bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     if (norm) *norm = nrm;
     return BURG_OK;
@@ -1648,24 +1678,23 @@ int burg_slab_residual(burg_ctx *c, const double *w, const double *wp, const dou
                     c->row0 - 1);
     if (int e = ensure_scratch(c)) return e;
     const size_t bytes = c->m() * sizeof(double), hb = 2 * (size_t)c->nx * sizeof(double);
-    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_d, wp, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_x, w, bytes, c->stream));
+    HIPCHK(h2d(c->d_d, wp, bytes, c->stream));
     // the halo rows go to a scratch buffer kept by the context (allocated on
     // first use: no hipMalloc / hipFree -- a device-wide sync -- per call)
     const double *d_halo = nullptr;
     if (halo_w) {
         if (!c->d_halo_rows)
             if (int e = dalloc(&c->d_halo_rows, 4 * (size_t)c->nx)) return e;
-        HIPCHK(hipMemcpyAsync(c->d_halo_rows, halo_w, hb, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(hipMemcpyAsync(c->d_halo_rows + 2 * c->nx, halo_wp, hb, hipMemcpyHostToDevice,
-                              c->stream));
+        HIPCHK(h2d(c->d_halo_rows, halo_w, hb, c->stream));
+        HIPCHK(h2d(c->d_halo_rows + 2 * c->nx, halo_wp, hb, c->stream));
         d_halo = c->d_halo_rows;
     }
     int rc = launch_residual(c->cf, c->d_x, c->d_d, c->d_r, c->d_partials, c->d_sumsq, d_halo,
                              d_halo ? d_halo + 2 * c->nx : nullptr, c->stream);
     double s = 0.0;
     if (rc == 0 &&
-        (hipMemcpyAsync(r, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        (d2h(r, c->d_r, bytes, c->stream) != hipSuccess ||
          hipMemcpyAsync(&s, c->d_sumsq, sizeof s, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
          hipStreamSynchronize(c->stream) != hipSuccess))
         rc = -3;
@@ -1681,10 +1710,10 @@ int burg_jvp(burg_ctx *c, const double *w, const double *x, double *y)
     if (!w || !x || !y) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
     const size_t bytes = c->m() * sizeof(double);
-    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_d, x, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_x, w, bytes, c->stream));
+    HIPCHK(h2d(c->d_d, x, bytes, c->stream));
     CHK(launch_jvp(c->cf, c->d_x, c->d_d, c->d_r, c->stream));
-    HIPCHK(hipMemcpyAsync(y, c->d_r, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(d2h(y, c->d_r, bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BURG_OK;
 }
@@ -1696,10 +1725,10 @@ int burg_block_solve(burg_ctx *c, const double *w, const double *rhs, double *de
     if (!w || !rhs || !delta) return fail(BURG_EINVAL, "null array");
     if (int e = ensure_scratch(c)) return e;
     const size_t bytes = c->m() * sizeof(double);
-    HIPCHK(hipMemcpyAsync(c->d_x, w, bytes, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_r, rhs, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_x, w, bytes, c->stream));
+    HIPCHK(h2d(c->d_r, rhs, bytes, c->stream));
     if (int e = block_solve(c, c->d_x, c->d_r, c->d_d)) return e;
-    HIPCHK(hipMemcpyAsync(delta, c->d_d, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(d2h(delta, c->d_d, bytes, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BURG_OK;
 }
@@ -1708,8 +1737,7 @@ int burg_upload_state(burg_ctx *c, const double *w)
 {
     if (int e = check_ready(c)) return e;
     if (!w) return fail(BURG_EINVAL, "null state");
-    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w, c->m() * sizeof(double),
-                          hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_state[c->cur], w, c->m() * sizeof(double), c->stream));
     if (!c->d_w0)
         if (int e = dalloc(&c->d_w0, c->m())) return e;
     HIPCHK(hipMemcpyAsync(c->d_w0, c->d_state[c->cur], c->m() * sizeof(double),
@@ -1722,8 +1750,7 @@ int burg_download_state(burg_ctx *c, double *w)
 {
     if (int e = check_ready(c)) return e;
     if (!w) return fail(BURG_EINVAL, "null state");
-    HIPCHK(hipMemcpyAsync(w, c->d_state[c->cur], c->m() * sizeof(double),
-                          hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(d2h(w, c->d_state[c->cur], c->m() * sizeof(double), c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return BURG_OK;
 }
@@ -1880,15 +1907,16 @@ static int check_device_ptr(const burg_ctx *c, const void *p, const char *what);
 
 // Columns col0 .. col0 + ncols - 1 of the resident trajectory (state
 // first + j * stride in column j) into the C-order (2n x ld_out) matrix `out`
-// at column offsets 0 .. ncols - 1: host memory (staged, pinned when it can
-// be registered) or, with out_on_device, device memory of this GPU.
+// at column offsets 0 .. ncols - 1: host memory (staged through the pinned
+// bounce buffers, hostxfer.hip) or, with out_on_device, device memory of this GPU.
 int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, int64_t ld_out,
                          int out_on_device)
 {
     BURG_TRACE("burg_trajectory_copy");
     if (int e = check_ready(c)) return e;
     const TrajRecord &tr = c->tr;
-    if (!tr.valid) return fail(BURG_ESTATE, "no trajectory resident (burg_trajectory_ex)");
+    if (!tr.valid || !c->sp_ready || !c->d_ring)
+        return fail(BURG_ESTATE, "no trajectory resident (burg_trajectory_ex)");
     if (!out) return fail(BURG_EINVAL, "null output");
     if (col0 < 0 || ncols < 0 || col0 + ncols > tr.count)
         return fail(BURG_EINVAL, "columns [%lld, %lld) outside the %lld retained", (long long)col0,
@@ -1906,7 +1934,6 @@ int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, 
     const int64_t j1 = col0 + ncols;
     int rc = BURG_OK;
     double *d_tr = nullptr;
-    bool registered = false;
     int S = 0;
     if (!out_on_device) {
         size_t freeb = 0, totalb = 0;
@@ -1914,28 +1941,26 @@ int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, 
         S = (int)std::min<int64_t>(ncols, 64);
         while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
         if (int e = dalloc(&d_tr, (size_t)S * m)) return e;
-        registered = hipHostRegister(out, m * (size_t)ld_out * sizeof(double),
-                                     hipHostRegisterDefault) == hipSuccess;
-        (void)hipGetLastError();
     }
     while (j < j1 && rc == BURG_OK) {
         double *dst = out_on_device ? out + (j - col0) : d_tr;
         const int ldo = out_on_device ? (int)ld_out : S;
+        const size_t cap = out_on_device ? m * (size_t)ld_out - (size_t)(j - col0) : (size_t)S * m;
         int n = 0;
         if (tr.ret0 && rel(j) == 0) {
             // the initial state: its copy (the working ring has moved on)
             const double *p0 = c->d_ret0;
-            if (launch_transpose(&p0, 1, m, dst, ldo, c->stream)) rc = fail(BURG_EHIP, "column copy failed");
+            if (launch_transpose(&p0, 1, m, dst, ldo, cap, bflag(c), c->stream))
+                rc = fail(BURG_EHIP, "column copy failed");
             n = 1;
         } else {
             n = (int)std::min<int64_t>(j1 - j, out_on_device ? INT32_MAX : S);
-            if (launch_ring_extract(ra, W, (int)rel(j), tr.stride, n, dst, ldo, c->stream))
+            if (launch_ring_extract(ra, W, (int)rel(j), tr.stride, n, dst, ldo, cap, c->stream))
                 rc = fail(BURG_EHIP, "ring extract launch failed");
         }
         if (rc == BURG_OK && !out_on_device &&
-            hipMemcpy2DAsync(out + (j - col0), (size_t)ld_out * sizeof(double), d_tr,
-                             (size_t)S * sizeof(double), (size_t)n * sizeof(double), m,
-                             hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+            d2h_2d(out + (j - col0), (size_t)ld_out * sizeof(double), d_tr,
+                   (size_t)S * sizeof(double), (size_t)n * sizeof(double), m, c->stream) != hipSuccess)
             rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
         if (rc == BURG_OK && !out_on_device && hipStreamSynchronize(c->stream) != hipSuccess)
             rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
@@ -1943,7 +1968,7 @@ int burg_trajectory_copy(burg_ctx *c, int64_t col0, int64_t ncols, double *out, 
     }
     if (rc == BURG_OK && hipStreamSynchronize(c->stream) != hipSuccess)
         rc = fail(BURG_EHIP, "snapshot copy failed: %s", hipGetErrorString(hipGetLastError()));
-    if (registered) (void)hipHostUnregister(out);
+    if (rc == BURG_OK) rc = check_bounds(c, "burg_trajectory_copy");
     dfree(d_tr);
     return rc;
 }
@@ -2024,9 +2049,9 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
     ch->engine = BURG_ENGINE_PIPE;
     // host copies of the grid's coefficient rows and of w0
     std::vector<double> ix(nx), iy(ny), w0(m);
-    HIPCHK(hipMemcpy(ix.data(), c->cf.inv_dx, sizeof(double) * nx, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(iy.data(), c->cf.inv_dy, sizeof(double) * ny, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(w0.data(), c->d_w0, sizeof(double) * m, hipMemcpyDeviceToHost));
+    HIPCHK(d2h(ix.data(), c->cf.inv_dx, sizeof(double) * nx, c->stream));
+    HIPCHK(d2h(iy.data(), c->cf.inv_dy, sizeof(double) * ny, c->stream));
+    HIPCHK(d2h(w0.data(), c->d_w0, sizeof(double) * m, c->stream));
     const size_t nc = ch->n(), dpl = (size_t)ny_pad * nx;  // child plane, one domain's rows
     std::vector<double> iyt((size_t)G * ny_pad), lbt((size_t)G * ny_pad), w0s(2 * nc, 1.0);
     for (int j = 0; j < G; ++j)
@@ -2037,7 +2062,6 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
     }
     double *d_srcb = nullptr, *d_tr = nullptr;
     d2 *d_colcb = nullptr;
-    bool registered = false;
     int S = 0;
     auto cleanup = [&]() {
         ch->ov_colc = nullptr;
@@ -2049,8 +2073,6 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
         ch->ring_entries = 0;
         ch->ring_maxed = false;
         ch->tr.valid = false;
-        if (registered)
-            for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(out.host[j]);
         dfree(d_srcb);
         dfree(d_colcb);
         dfree(d_tr);
@@ -2091,19 +2113,9 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
                 S = (int)std::min<int64_t>(ncols, 64);
                 while (S > 1 && (size_t)S * m * sizeof(double) > freeb / 3) S /= 2;
                 if ((rc = dalloc(&d_tr, (size_t)S * m))) break;
-                registered = true;
-                for (int j = 0; j < nmu; ++j)
-                    if (hipHostRegister(out.host[j], m * out.ld_host * sizeof(double),
-                                        hipHostRegisterDefault) != hipSuccess) {
-                        (void)hipGetLastError();
-                        for (int i = 0; i < j; ++i) (void)hipHostUnregister(out.host[i]);
-                        registered = false;
-                        break;
-                    }
             }
         }
-        if (hipMemcpyAsync(d_srcb, srcg.data(), sizeof(double) * G * nx, hipMemcpyHostToDevice,
-                           ch->stream) != hipSuccess ||
+        if (h2d(d_srcb, srcg.data(), sizeof(double) * G * nx, ch->stream) != hipSuccess ||
             launch_colc_batch(ch->cf, G, d_srcb, (int)ncolp, d_colcb, ch->stream) != 0) {
             rc = fail(BURG_EHIP, "side-by-side sweep: column tables: %s",
                       hipGetErrorString(hipGetLastError()));
@@ -2143,10 +2155,11 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
             if (out.dev) {
                 double *dst = out.dev + (size_t)(g0 + j) * ncols;
                 const int ldo = (int)out.ld_dev;
+                const size_t cap = m * (size_t)out.ld_dev - (size_t)(g0 + j) * ncols;
                 const double *p0 = c->d_w0;
-                if (launch_transpose(&p0, 1, m, dst, ldo, ch->stream) ||
+                if (launch_transpose(&p0, 1, m, dst, ldo, cap, bflag(ch), ch->stream) ||
                     (ncols > 1 && launch_ring_extract(va, W, snap_every, snap_every, (int)(ncols - 1),
-                                                      dst + 1, ldo, ch->stream)))
+                                                      dst + 1, ldo, cap - 1, ch->stream)))
                     rc = fail(BURG_EHIP, "sweep snapshot extract failed");
                 continue;
             }
@@ -2156,17 +2169,17 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
                 const int cnt = (int)std::min<int64_t>(S, ncols - k0);
                 int e = 0;
                 if (k0 == 0) {
-                    e = launch_transpose(&p0, 1, m, d_tr, S, ch->stream);
+                    e = launch_transpose(&p0, 1, m, d_tr, S, (size_t)S * m, bflag(ch), ch->stream);
                     if (!e && cnt > 1)
                         e = launch_ring_extract(va, W, snap_every, snap_every, cnt - 1, d_tr + 1, S,
-                                                ch->stream);
+                                                (size_t)S * m - 1, ch->stream);
                 } else {
                     e = launch_ring_extract(va, W, (int)(k0 * snap_every), snap_every, cnt, d_tr, S,
-                                            ch->stream);
+                                            (size_t)S * m, ch->stream);
                 }
-                if (e || hipMemcpy2DAsync(dst + k0, (size_t)out.ld_host * sizeof(double), d_tr,
-                                          (size_t)S * sizeof(double), (size_t)cnt * sizeof(double),
-                                          m, hipMemcpyDeviceToHost, ch->stream) != hipSuccess ||
+                if (e || d2h_2d(dst + k0, (size_t)out.ld_host * sizeof(double), d_tr,
+                                (size_t)S * sizeof(double), (size_t)cnt * sizeof(double), m,
+                                ch->stream) != hipSuccess ||
                     hipStreamSynchronize(ch->stream) != hipSuccess)
                     rc = fail(BURG_EHIP, "sweep snapshot copy failed");
             }
@@ -2178,6 +2191,7 @@ static int sweep_side_by_side(burg_ctx *c, int nmu, const double *src_b, const d
         flush_ms += t;
         (void)hipEventDestroy(f0);
         (void)hipEventDestroy(f1);
+        if (rc == BURG_OK) rc = check_bounds(ch, "side-by-side sweep");
         if (rc == BURG_OK && g0 + nb == nmu) {
             // the last trajectory's final state becomes the parent's resident state
             const double *fs = ch->d_state[ch->cur] + (size_t)(nb - 1) * dpl;
@@ -2263,7 +2277,6 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
     // per-trajectory coefficient tables (this slab's rows of lbc)
     double *d_srcb = nullptr, *d_lbcb = nullptr, *d_tr = nullptr;
     d2 *d_colcb = nullptr;
-    bool registered = false;
     int rc = BURG_OK;
     auto cleanup = [&]() {
         c->sw_T = 0;
@@ -2272,8 +2285,6 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
         c->ov_colc = nullptr;
         c->ov_lbc = nullptr;
         (void)hipStreamSynchronize(c->stream);
-        if (registered)
-            for (int j = 0; j < nmu; ++j) (void)hipHostUnregister(snaps[j]);
         dfree(d_srcb);
         dfree(d_lbcb);
         dfree(d_colcb);
@@ -2284,12 +2295,15 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
         cleanup();
         return rc;
     }
-    HIPCHK(hipMemcpyAsync(d_srcb, src_b, sizeof(double) * nmu * c->nx, hipMemcpyHostToDevice,
-                          c->stream));
-    HIPCHK(hipMemcpy2DAsync(d_lbcb, sizeof(double) * c->nrows, lbc_b + c->row0,
-                            sizeof(double) * c->ny_total, sizeof(double) * c->nrows, nmu,
-                            hipMemcpyHostToDevice, c->stream));
-    CHK(launch_colc_batch(c->cf, nmu, d_srcb, (int)ncolp, d_colcb, c->stream));
+    // (a failure from here on still goes through cleanup: no device buffer leaks)
+    if (h2d(d_srcb, src_b, sizeof(double) * nmu * c->nx, c->stream) != hipSuccess ||
+        h2d_2d(d_lbcb, sizeof(double) * c->nrows, lbc_b + c->row0, sizeof(double) * c->ny_total,
+               sizeof(double) * c->nrows, nmu, c->stream) != hipSuccess ||
+        launch_colc_batch(c->cf, nmu, d_srcb, (int)ncolp, d_colcb, c->stream) != 0) {
+        rc = fail(BURG_EHIP, "burg_sweep: coefficient tables: %s", hipGetErrorString(hipGetLastError()));
+        cleanup();
+        return rc;
+    }
 
     // trajectories per launch: as many as the ring budget (a third of free
     // HBM) holds -- the sweep's states all stay resident until extracted
@@ -2323,15 +2337,6 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
             cleanup();
             return rc;
         }
-        registered = true;
-        for (int j = 0; j < nmu; ++j)
-            if (hipHostRegister(snaps[j], m * ld_snaps * sizeof(double), hipHostRegisterDefault) !=
-                hipSuccess) {
-                (void)hipGetLastError();
-                for (int i = 0; i < j; ++i) (void)hipHostUnregister(snaps[i]);
-                registered = false;
-                break;
-            }
     }
     float ms = 0.f, flush_ms = 0.f;
     hipEvent_t f0 = nullptr, f1 = nullptr;
@@ -2362,12 +2367,13 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
             // straight into the device matrix: column 0 = w0, then the states
             for (int j = 0; j < nb && rc == BURG_OK; ++j) {
                 double *dst = out.dev + (size_t)(g0 + j) * ncols;
+                const size_t cap = m * (size_t)out.ld_dev - (size_t)(g0 + j) * ncols;
                 const double *p0 = c->d_w0;
-                if (launch_transpose(&p0, 1, m, dst, (int)out.ld_dev, c->stream) ||
+                if (launch_transpose(&p0, 1, m, dst, (int)out.ld_dev, cap, bflag(c), c->stream) ||
                     (ncols > 1 && launch_ring_extract(stream_args(c, L, 0, 0), W,
                                                       (int)(j * T + snap_every), snap_every,
                                                       (int)(ncols - 1), dst + 1, (int)out.ld_dev,
-                                                      c->stream)))
+                                                      cap - 1, c->stream)))
                     rc = fail(BURG_EHIP, "snapshot extract failed");
             }
             continue;
@@ -2377,8 +2383,8 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
         for (int j = 0; j < nb && rc == BURG_OK; ++j) {
             double *dst = snaps[g0 + j];
             // column 0 = the initial state
-            if (hipMemcpy2DAsync(dst, (size_t)ld_snaps * sizeof(double), c->d_w0, sizeof(double),
-                                 sizeof(double), m, hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+            if (d2h_2d(dst, (size_t)ld_snaps * sizeof(double), c->d_w0, sizeof(double),
+                       sizeof(double), m, c->stream) != hipSuccess) {
                 rc = fail(BURG_EHIP, "snapshot copy failed");
                 break;
             }
@@ -2387,10 +2393,9 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
                 const int n = (int)std::min<int64_t>(S, ncols - k0);
                 if (launch_ring_extract(stream_args(c, L, 0, 0), W,
                                         (int)(j * T + k0 * snap_every), snap_every, n, d_tr, n,
-                                        c->stream) ||
-                    hipMemcpy2DAsync(dst + k0, (size_t)ld_snaps * sizeof(double), d_tr,
-                                     n * sizeof(double), n * sizeof(double), m,
-                                     hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+                                        (size_t)S * m, c->stream) ||
+                    d2h_2d(dst + k0, (size_t)ld_snaps * sizeof(double), d_tr,
+                           n * sizeof(double), n * sizeof(double), m, c->stream) != hipSuccess) {
                     rc = fail(BURG_EHIP, "snapshot extract failed");
                     break;
                 }
@@ -2405,10 +2410,11 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
     if (rc == BURG_OK) {
         // the last trajectory's final state becomes the resident state
         rc = launch_ring_extract(stream_args(c, L, 0, 0), W, last_nb * T, 1, 1,
-                                 c->d_state[c->cur ^ 1], 1, c->stream);
+                                 c->d_state[c->cur ^ 1], 1, m, c->stream);
         if (rc) rc = fail(BURG_EHIP, "ring extract launch failed");
         else c->cur ^= 1;
     }
+    if (rc == BURG_OK) rc = check_bounds(c, "burg_sweep");
     if (rc == BURG_OK) rc = stream_stats_end(c, st, (int64_t)nmu * T, launches);
     if (st) {
         st->loop_ms = ms;
@@ -2456,11 +2462,9 @@ int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const doubl
     const size_t m = c->m(), n = c->n();
     const size_t blk = (size_t)n_pod * n;  // one snapshot's C rows
     double *d_b = nullptr, *d_bt = nullptr, *d_w = nullptr, *d_cb = nullptr;
-    bool registered = false;
     int rc = BURG_OK;
     auto cleanup = [&]() {
         (void)hipStreamSynchronize(c->stream);
-        if (registered) (void)hipHostUnregister(C);
         dfree(d_b);
         dfree(d_bt);
         dfree(d_w);
@@ -2471,20 +2475,18 @@ int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const doubl
         cleanup();
         return rc;
     }
-    HIPCHK(hipMemcpyAsync(d_b, basis, sizeof(double) * m * n_pod, hipMemcpyHostToDevice,
-                          c->stream));
-    CHK(launch_basis_transpose(d_b, d_bt, m, n_pod, c->stream));
-    registered = hipHostRegister(C, sizeof(double) * blk * n_snaps, hipHostRegisterDefault) ==
-                 hipSuccess;
-    (void)hipGetLastError();
+    if (h2d(d_b, basis, sizeof(double) * m * n_pod, c->stream) != hipSuccess ||
+        launch_basis_transpose(d_b, d_bt, m, n_pod, c->stream) != 0) {
+        rc = fail(BURG_EHIP, "burg_ecsw_matrix: basis upload: %s", hipGetErrorString(hipGetLastError()));
+        cleanup();
+        return rc;
+    }
     float kern = 0.f, copy = 0.f;
     hipEvent_t e2 = nullptr;
     (void)hipEventCreate(&e2);
     for (int i = 0; i < n_snaps && rc == BURG_OK; ++i) {
-        if (hipMemcpyAsync(d_w, states + (size_t)i * m, sizeof(double) * m, hipMemcpyHostToDevice,
-                           c->stream) != hipSuccess ||
-            hipMemcpyAsync(d_w + m, prev_states + (size_t)i * m, sizeof(double) * m,
-                           hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+        if (h2d(d_w, states + (size_t)i * m, sizeof(double) * m, c->stream) != hipSuccess ||
+            h2d(d_w + m, prev_states + (size_t)i * m, sizeof(double) * m, c->stream) != hipSuccess) {
             rc = fail(BURG_EHIP, "state upload failed");
             break;
         }
@@ -2494,8 +2496,7 @@ int burg_ecsw_matrix(burg_ctx *c, int n_snaps, const double *states, const doubl
             break;
         }
         (void)hipEventRecord(c->ev1, c->stream);
-        if (hipMemcpyAsync(C + (size_t)i * blk, d_cb, sizeof(double) * blk,
-                           hipMemcpyDeviceToHost, c->stream) != hipSuccess) {
+        if (d2h(C + (size_t)i * blk, d_cb, sizeof(double) * blk, c->stream) != hipSuccess) {
             rc = fail(BURG_EHIP, "C block copy failed");
             break;
         }
@@ -2584,7 +2585,6 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
     // copied as a 2D block into columns [col0, col0+S) of the host matrix.
     int S = 0;
     double *d_chunk = nullptr, *d_tr = nullptr;
-    bool registered = false;
     if (snaps) {
         size_t freeb = 0, totalb = 0;
         HIPCHK(hipMemGetInfo(&freeb, &totalb));
@@ -2596,9 +2596,6 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
             dfree(d_chunk);
             return e;
         }
-        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
-                                     hipHostRegisterDefault) == hipSuccess;
-        (void)hipGetLastError();
     }
     std::vector<const double *> slots;
     int64_t col0 = 0;
@@ -2610,10 +2607,9 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
         if (slots.empty()) return 0;
         HIPCHK(hipEventRecord(f0, c->stream));
         CHK(launch_transpose(slots.data(), (int)slots.size(), m, d_tr, (int)slots.size(),
-                             c->stream));
-        HIPCHK(hipMemcpy2DAsync(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
-                                slots.size() * sizeof(double), slots.size() * sizeof(double), m,
-                                hipMemcpyDeviceToHost, c->stream));
+                             (size_t)S * m, bflag(c), c->stream));
+        HIPCHK(d2h_2d(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
+                      slots.size() * sizeof(double), slots.size() * sizeof(double), m, c->stream));
         HIPCHK(hipEventRecord(f1, c->stream));
         HIPCHK(hipEventSynchronize(f1));
         float t = 0.f;
@@ -2633,7 +2629,7 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
 
     int rc = BURG_OK;
     HIPCHK(hipMemsetAsync(c->d_stats, 0, sizeof(DevStats), c->stream));
-    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(h2d(c->d_state[c->cur], w0, bytes, c->stream));
     if (snaps) rc = keep(c->d_state[c->cur]);
     int64_t nupd = 0;
     int maxupd = 0;
@@ -2680,6 +2676,7 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
         }
     }
     if (rc == BURG_OK && snaps) rc = flush();
+    if (rc == BURG_OK) rc = check_bounds(c, "burg_run");
     if (rc == BURG_OK) rc = read_stats(c, st);
     if (st) {
         st->loop_ms = loop_ms;
@@ -2691,7 +2688,6 @@ int burg_run(burg_ctx *c, const double *w0, int num_steps, int solver, int newto
     }
     collect_profile(c, st);
     (void)hipStreamSynchronize(c->stream);
-    if (registered) (void)hipHostUnregister(snaps);
     dfree(d_chunk);
     dfree(d_tr);
     (void)hipEventDestroy(f0);
@@ -2828,8 +2824,7 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
     // the trajectory: one launch, every state in the ring
     const auto t_start = std::chrono::steady_clock::now();
     stream_stats_begin(c);
-    HIPCHK(hipMemcpyAsync(c->d_state[c->cur], w0, m * sizeof(double), hipMemcpyHostToDevice,
-                          c->stream));
+    HIPCHK(h2d(c->d_state[c->cur], w0, m * sizeof(double), c->stream));
     CHK(launch_ring_load(stream_args(c, L, 0, 0), W, c->d_state[c->cur], c->stream));
     float ms = 0.f;
     if ((rc = stream_launch(c, L, 0, num_steps, &ms))) {
@@ -2853,7 +2848,7 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         double *dst = d_blk + (size_t)bi * R * ncols;
         (void)hipEventRecord(f0, c->stream);
         if (launch_ring_extract_rows(stream_args(c, L, 0, 0), W, e0, ne, 0, snap_every, (int)ncols,
-                                     dst, c->stream) ||
+                                     dst, R * (size_t)ncols, c->stream) ||
             hipMemcpyAsync(h_blk[bi], dst, ne * row_bytes, hipMemcpyDeviceToHost, c->stream) !=
                 hipSuccess) {
             rc = fail(BURG_EHIP, "snapshot row block copy failed");
@@ -2887,10 +2882,11 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
     if (rc == BURG_OK) {
         const long long o_last = 0;
         rc = launch_ring_extract(stream_args(c, L, o_last, 0), W, num_steps, 1, 1,
-                                 c->d_state[c->cur ^ 1], 1, c->stream);
+                                 c->d_state[c->cur ^ 1], 1, m, c->stream);
         if (rc) rc = fail(BURG_EHIP, "ring extract launch failed");
         else c->cur ^= 1;
     }
+    if (rc == BURG_OK) rc = check_bounds(c, "burg_run_npy");
     if (rc == BURG_OK) rc = stream_stats_end(c, st, num_steps, 1);
     if (st) {
         st->loop_ms = ms;
@@ -2943,13 +2939,11 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     // rocSOLVER potrf/potrs (BURG_LSPG_SOLVE=kernel|lib)
     const char *solve_env = getenv("BURG_LSPG_SOLVE");
     const bool lib_solve = !(solve_env && std::strcmp(solve_env, "kernel") == 0);
-    bool registered = false;
     std::vector<hipEvent_t> evs;
     auto cleanup = [&]() {
         (void)hipStreamSynchronize(c->stream);
         if (rh) rocblas_destroy_handle(rh);
         dfree(d_info), dfree(d_d0);
-        if (registered) (void)hipHostUnregister(snaps);
         for (auto e : evs) (void)hipEventDestroy(e);
         dfree(d_b), dfree(d_bt), dfree(d_btT), dfree(d_bk), dfree(d_w), dfree(d_wT), dfree(d_wp), dfree(d_y);
         dfree(d_part), dfree(d_G), dfree(d_err), dfree(d_chunk), dfree(d_tr);
@@ -2982,7 +2976,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     } while (0)
     LCHK(dalloc(&d_b, m * n_pod));
     LCHK(dalloc(&d_bt, m * n_pod));
-    LHIP(hipMemcpyAsync(d_b, basis, sizeof(double) * m * n_pod, hipMemcpyHostToDevice, c->stream));
+    LHIP(h2d(d_b, basis, sizeof(double) * m * n_pod, c->stream));
     LLAUNCH(launch_basis_transpose(d_b, d_bt, m, n_pod, c->stream));
     LHIP(hipStreamSynchronize(c->stream));
     dfree(d_b);
@@ -3025,9 +3019,6 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
         while (S > 1 && (size_t)S * 2 * m * sizeof(double) > freeb / 4) S /= 2;
         LCHK(dalloc(&d_chunk, (size_t)S * m));
         LCHK(dalloc(&d_tr, (size_t)S * m));
-        registered = hipHostRegister(snaps, (size_t)m * ld_snaps * sizeof(double),
-                                     hipHostRegisterDefault) == hipSuccess;
-        (void)hipGetLastError();
     }
     std::vector<double> yh((size_t)n_pod);
     for (int k = 0; k < 8; ++k) {
@@ -3045,10 +3036,9 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
         if (slots.empty()) return 0;
         HIPCHK(hipEventRecord(evs[6], c->stream));
         CHK(launch_transpose(slots.data(), (int)slots.size(), m, d_tr, (int)slots.size(),
-                             c->stream));
-        HIPCHK(hipMemcpy2DAsync(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
-                                slots.size() * sizeof(double), slots.size() * sizeof(double), m,
-                                hipMemcpyDeviceToHost, c->stream));
+                             (size_t)S * m, bflag(c), c->stream));
+        HIPCHK(d2h_2d(snaps + col0, (size_t)ld_snaps * sizeof(double), d_tr,
+                      slots.size() * sizeof(double), slots.size() * sizeof(double), m, c->stream));
         HIPCHK(hipEventRecord(evs[7], c->stream));
         HIPCHK(hipEventSynchronize(evs[7]));
         flush_ms += elapsed(6, 7);
@@ -3067,9 +3057,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
                 if (int e = flush()) return e;
         }
         if (red_coords) {
-            HIPCHK(hipMemcpyAsync(yh.data(), d_y, sizeof(double) * n_pod, hipMemcpyDeviceToHost,
-                                  c->stream));
-            HIPCHK(hipStreamSynchronize(c->stream));
+            HIPCHK(d2h(yh.data(), d_y, sizeof(double) * n_pod, c->stream));
             for (int k = 0; k < n_pod; ++k) red_coords[(size_t)k * ld_red + j] = yh[k];
         }
         return 0;
@@ -3090,7 +3078,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     };
 
     const auto t0 = std::chrono::steady_clock::now();
-    LHIP(hipMemcpyAsync(d_wp, w0, m * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    LHIP(h2d(d_wp, w0, m * sizeof(double), c->stream));
     LLAUNCH(launch_lspg_project(d_bt, d_wp, n_pod, m, d_part, d_y, c->stream));  // y0 = V^T w0
     LCHK(expand());                                                              // w0 = V y0
     LCHK(keep(0));
@@ -3139,6 +3127,7 @@ int burg_lspg(burg_ctx *c, const double *w0, int num_steps, int n_pod, const dou
     }
     if (rc == BURG_OK) LCHK(flush());
     LHIP(hipStreamSynchronize(c->stream));
+    if (rc == BURG_OK) LCHK(check_bounds(c, "burg_lspg"));
     const double loop_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (st) {
@@ -3219,7 +3208,7 @@ static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool sna
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     if (!snaps_on_device &&
-        hipMemcpyAsync(d_s, snaps, sizeof(double) * mm * ns, hipMemcpyHostToDevice, st) != hipSuccess) {
+        h2d(d_s, snaps, sizeof(double) * mm * ns, st) != hipSuccess) {
         cleanup();
         return fail(BURG_EHIP, "burg_pod: snapshot upload failed");
     }
@@ -3229,8 +3218,7 @@ static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool sna
             cleanup();
             return rc;
         }
-        if (hipMemcpyAsync(d_om, omega, sizeof(double) * ns * nrand, hipMemcpyHostToDevice, st) !=
-            hipSuccess) {
+        if (h2d(d_om, omega, sizeof(double) * ns * nrand, st) != hipSuccess) {
             cleanup();
             return fail(BURG_EHIP, "burg_pod_rsvd: omega upload failed");
         }
@@ -3246,8 +3234,8 @@ static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool sna
         return fail(r == -1 ? BURG_EINVAL : r == -5 ? BURG_ENOMEM : r == -6 ? BURG_ENOCONV : BURG_EHIP,
                     "burg_pod: %s", msg);
     }
-    if (hipMemcpyAsync(U, d_u, sizeof(double) * mm * k, hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipMemcpyAsync(sigma, d_sig, sizeof(double) * k, hipMemcpyDeviceToHost, st) != hipSuccess ||
+    if (d2h(U, d_u, sizeof(double) * mm * k, st) != hipSuccess ||
+        d2h(sigma, d_sig, sizeof(double) * k, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess) {
         cleanup();
         return fail(BURG_EHIP, "burg_pod: result download failed");
@@ -3258,6 +3246,145 @@ static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool sna
         *ms = t;
     }
     cleanup();
+    return BURG_OK;
+}
+
+const char *burg_build_id(void) { return BURG_BUILD_ID; }
+
+// Host-only replay of every ring entry the pipe engine's trajectory kernels
+// form (include/burgers.h).  The walks below are the
+// kernels' own: ring_load_kernel and ring_extract_kernel call ring_pos, the
+// compute waves advance pw per diagonal from RetCursor::next at each block
+// (retained windows) or from origin with a wrap at L, the loader wave reads
+// diagonal d - W for d in blocks of U.  Cells are tracked per (entry, lane):
+// lane l of diagonal s holds local time s - l.
+int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t *report)
+{
+    if (!report) return fail(BURG_EINVAL, "null report");
+    if (!pipe_width_supported(W)) return fail(BURG_EINVAL, "W=%d: not a pipe-engine width", W);
+    if (num_steps < 1 || snap_every < 1 || ring_cap < 0)
+        return fail(BURG_EINVAL, "num_steps, snap_every >= 1, ring_cap >= 0");
+    const int U = pipe_block_of(W);
+    const int k = snap_every;
+    TrajMap mp;
+    long long K = num_steps;
+    if (k >= 2 && (long long)k * W >= W + 64) {
+        const long long cap = ring_cap > 0 ? (long long)ring_cap * W + 128 : LLONG_MAX;
+        if (!retained_layout(W, num_steps, k, cap, &mp))
+            return fail(BURG_ESHAPE, "no retained layout for W=%d, %d steps, snap_every %d", W,
+                        num_steps, k);
+    } else {
+        long long C = std::min<long long>(num_steps, ((1 << 21) - 4096) / W - 1);
+        if (ring_cap > 0) C = std::min<long long>(C, ring_cap);
+        K = std::min<long long>(num_steps, std::max<long long>(C, ((1 << 21) - 4096) / W - 1));
+        mp = TrajMap{};
+        mp.L = C * W + W + 96;
+        mp.Lt = ring_stride(mp.L);
+    }
+    struct RA {
+        long long origin, L;
+        int ret_k, ret_n;
+        long long ret_base;
+    } ra{mp.origin, mp.L, mp.k, mp.n, mp.base};
+    const bool ret = mp.k > 0;
+    const long long Lt = mp.Lt, KW = K * W;
+    const long long total = KW + kWave - 1;  // diagonals of the launch
+    int64_t acc = 0, maxe = -1, oob = 0, mism = 0, over = 0, early = 0;
+    auto pos = [&](long long s) { return ring_pos(s, mp.origin, mp.L, W, mp.k, mp.n, mp.base); };
+    auto chk = [&](long long e, long long s, bool compare) {
+        ++acc;
+        maxe = std::max<int64_t>(maxe, e);
+        if (e < 0 || e >= Lt) ++oob;
+        if (compare && e != pos(s)) ++mism;
+    };
+    // last writer (diagonal) of each (entry, lane); writer diagonal of each entry
+    const long long NONE = LLONG_MIN;
+    std::vector<long long> cell((size_t)Lt * kWave, NONE), ewr((size_t)Lt, NONE);
+    auto write = [&](long long e, long long s, int lane) {
+        if (e < 0 || e >= Lt) return;
+        cell[(size_t)e * kWave + lane] = s;
+    };
+    auto write_entry = [&](long long e, long long s) {
+        if (e < 0 || e >= Lt) return;
+        // the content of diagonal p is read back (previous state) at p + W:
+        // a later store to its entry before that would corrupt the read
+        if (ewr[e] != NONE && ewr[e] != s && ewr[e] + W > s) ++early;
+        ewr[e] = std::max(ewr[e], s);
+    };
+    // initial state (ring_load_kernel): state 0 of (lane, column cl) at diagonal cl + lane - W
+    for (long long s = -W; s < kWave - 1; ++s) {
+        chk(pos(s), s, false);
+        write_entry(pos(s), s);
+    }
+    for (int lane = 0; lane < kWave; ++lane)
+        for (int cl = 0; cl < W; ++cl) write(pos((long long)cl + lane - W), (long long)cl + lane - W, lane);
+    // compute waves: one store per diagonal (lanes with local time in [0, KW))
+    {
+        RetCursor rc;
+        rc.init(ra, W, 0);
+        unsigned pw = (unsigned)mp.origin;
+        const unsigned Lu = (unsigned)mp.L;
+        for (long long sb = 0; sb < total; sb += U) {
+            if (ret) pw = rc.next(ra, W, U);
+            for (int u = 0; u < U; ++u) {
+                const long long s = sb + u;
+                const long long l0 = std::max<long long>(0, s - KW + 1), l1 = std::min<long long>(kWave - 1, s);
+                if (l0 <= l1) {  // some lane stores
+                    chk(pw, s, true);
+                    write_entry(pw, s);
+                    for (long long l = l0; l <= l1; ++l) write(pw, s, (int)l);
+                }
+                pw = pw + 1 == Lu ? 0u : pw + 1;
+            }
+        }
+    }
+    // loader wave (wide tiles): window slot of diagonal d <- entry of d - W
+    if (W > 16) {
+        RetCursor rc;
+        rc.init(ra, W, -W);
+        const long long tl = (total + U - 1) / U * U;
+        for (long long nf = 0; nf < tl; nf += U) {
+            long long e;
+            if (ret) {
+                e = rc.next(ra, W, U);
+            } else {
+                e = (mp.origin + nf - W) % mp.L;
+                e = e < 0 ? e + mp.L : e;
+            }
+            for (int u = 0; u < U; ++u) {
+                chk(e, nf - W + u, nf - W + u < total);
+                e = e + 1 == mp.L ? 0 : e + 1;
+            }
+        }
+    }
+    // the retained states (burg_trajectory_copy -> ring_extract_kernel): every
+    // cell must still hold the diagonal that produced it
+    std::vector<long long> states;
+    if (ret) {
+        for (int j = 1; j <= mp.n; ++j) states.push_back((long long)j * k);  // (state 0: d_ret0)
+    } else {
+        long long r0 = 0;
+        while (r0 <= K && (r0 - 1) * W + mp.L <= K * W + 62) ++r0;
+        const long long f = (r0 + k - 1) / k * k;
+        for (long long q = f; q <= K; q += k) states.push_back(q);
+    }
+    for (long long q : states)
+        for (int lane = 0; lane < kWave; ++lane)
+            for (int cl = 0; cl < W; ++cl) {
+                const long long s = (q - 1) * W + cl + lane;
+                const long long e = pos(s);
+                chk(e, s, false);
+                if (e >= 0 && e < Lt && cell[(size_t)e * kWave + lane] != s) ++over;
+            }
+    report[0] = acc;
+    report[1] = maxe;
+    report[2] = Lt;
+    report[3] = oob;
+    report[4] = mism;
+    report[5] = over;
+    report[6] = early;
+    report[7] = (int64_t)states.size() + (ret ? 1 : 0);
+    report[8] = ret ? k : (k >= 2 ? k : 1);
     return BURG_OK;
 }
 

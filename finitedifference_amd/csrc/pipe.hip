@@ -310,35 +310,7 @@ __device__ __forceinline__ long long now_rt() { return (long long)__builtin_amdg
 // through a VGPR select and a vector compare)
 __device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballot_w64(b) != 0; }
 
-// Walk of a tile's diagonals one block of U at a time through the retained
-// windows of ring_pos (burg_internal.h; a.ret_k > 0): entry of the block's
-// first diagonal, in scalar registers, advanced per block without divisions.
-// The windows, the working ring's wrap (L a multiple of U, origin 0) and the
-// blocks all start on multiples of U, so a block's U diagonals are U
-// consecutive entries.  s0: first diagonal of the walk, <= 0.
-struct RetCursor {
-    int j, o;    // window index, diagonal - (window j's first diagonal)
-    unsigned w;  // working-ring position of the next diagonal outside a window
-    __device__ void init(const PipeArgs &a, int W, int s0)
-    {
-        j = 0;
-        o = s0 - (a.ret_k - 1) * W;
-        long long e = (a.origin + s0) % a.L;
-        w = (unsigned)(e < 0 ? e + a.L : e);
-    }
-    __device__ unsigned next(const PipeArgs &a, int W, int U)
-    {
-        const bool inw = (o >= 0) & (o < W + 64) & (j < a.ret_n);
-        const unsigned e = inw ? (unsigned)a.ret_base + (unsigned)(j * (W + 64) + o) : w;
-        if (!inw) w = w + U >= (unsigned)a.L ? w + U - (unsigned)a.L : w + U;
-        o += U;
-        if (o == a.ret_k * W) {
-            o = 0;
-            ++j;
-        }
-        return e;
-    }
-};
+// (RetCursor, the retained-window walk: burg_internal.h)
 
 
 // LDS accesses that must not be cached in registers or merged (polled / handed
@@ -1527,6 +1499,23 @@ int pipe_per_cu_opt(int W)
 }  // namespace
 
 bool pipe_width_supported(int W) { return pipe_fn(W, false) != nullptr; }
+
+// diagonals per block of the trajectory kernel (its ring walk advances per
+// block; burg_ring_audit replays it)
+int pipe_block_of(int W)
+{
+    switch (W) {
+    case 8: return BURG_NARROW_U < 8 ? BURG_NARROW_U : 8;
+    case 16: return BURG_NARROW_U < 16 ? BURG_NARROW_U : 16;
+    case 32: return uw_of<32>();
+    case 64: return uw_of<64>();
+    case 128: return uw_of<128>();
+    case 256: return uw_of<256>();
+    case 512: return uw_of<512>();
+    case 1024: return uw_of<1024>();
+    default: return 0;
+    }
+}
 bool pipe_sweep_width_supported(int W) { return pipe_fn(W, true) != nullptr; }
 
 // resident workgroups of the pipe kernel (sweep = the burg_sweep variant,

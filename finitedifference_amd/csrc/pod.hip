@@ -1154,15 +1154,13 @@ int pod_rsvd_mfma(hipStream_t st, size_t m, int ns, const double *d_s, int k, in
         RS(orth_rows(h, st, nsz, R, Rp, z, g, tau, info, work, &tmp, &hh), "orth B^T");
         n_householder += hh;
         TS(ts_gemm_tn(st, z, Rp, nsz, Rp, b, Rp, Rp, g, Rp, work), "Q_b^T.B^T");
-        static bool lds_set = false;
-        if (!lds_set) {
-            if (hipFuncSetAttribute((const void *)jacobi_svd_kernel,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)jacobi_lds_bytes(128)) != hipSuccess) {
-                cleanup();
-                return err("jacobi LDS", 0);
-            }
-            lds_set = true;
+        // (set on every call: the attribute is per device, and a
+        // function-local "done" flag is neither per device nor thread-safe)
+        if (hipFuncSetAttribute((const void *)jacobi_svd_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)jacobi_lds_bytes(128)) != hipSuccess) {
+            cleanup();
+            return err("jacobi LDS", 0);
         }
         hipLaunchKernelGGL(jacobi_svd_kernel, dim3(1), dim3(kJT), jacobi_lds_bytes(R), st,
                            (const double *)g, Rp, R, ub, sv, (int *)info);
@@ -1189,7 +1187,11 @@ int pod_rsvd_mfma(hipStream_t st, size_t m, int ns, const double *d_s, int k, in
     }
     cleanup();
     if (hinfo != 0) {
-        snprintf(msg, msglen, "rocsolver_dgesvd did not converge (info=%d)", (int)hinfo);
+        if (ssvd && std::strcmp(ssvd, "rocsolver") == 0)
+            snprintf(msg, msglen, "rocsolver_dgesvd did not converge (info=%d)", (int)hinfo);
+        else
+            snprintf(msg, msglen, "one-sided Jacobi SVD of the %d x %d sketch did not converge "
+                     "within its sweep cap (info=%d)", R, R, (int)hinfo);
         return -6;
     }
     return 0;

@@ -285,7 +285,8 @@ struct StatePtrs {
 };
 
 __global__ __launch_bounds__(256) void transpose_kernel(StatePtrs sp, int nstates, size_t m,
-                                                        double *out, int ldo)
+                                                        double *out, int ldo, size_t out_elems,
+                                                        unsigned *flag)
 {
     __shared__ double tile[64][65];
     const size_t i0 = (size_t)blockIdx.x * 64;
@@ -297,7 +298,11 @@ __global__ __launch_bounds__(256) void transpose_kernel(StatePtrs sp, int nstate
     __syncthreads();
     for (int ii = ty; ii < 64; ii += 4) {
         const size_t i = i0 + ii;
-        if (i < m && tx < nstates) out[i * (size_t)ldo + tx] = tile[tx][ii];
+        if (i < m && tx < nstates) {
+            const size_t o = i * (size_t)ldo + tx;
+            if (o < out_elems) out[o] = tile[tx][ii];
+            else if (flag) atomicOr(flag, 2u);
+        }
     }
 }
 
@@ -392,13 +397,15 @@ int launch_axpy_neg(double *w, const double *d, size_t m, hipStream_t st)
 }
 
 int launch_transpose(const double *const *states, int nstates, size_t m, double *out,
-                     int ldo, hipStream_t st)
+                     int ldo, size_t out_elems, unsigned *flag, hipStream_t st)
 {
     for (int j0 = 0; j0 < nstates; j0 += kMaxStates) {
         StatePtrs sp{};
         const int cnt = nstates - j0 < kMaxStates ? nstates - j0 : kMaxStates;
         for (int j = 0; j < cnt; ++j) sp.p[j] = states[j0 + j];
-        transpose_kernel<<<(unsigned)((m + 63) / 64), 256, 0, st>>>(sp, cnt, m, out + j0, ldo);
+        if (out_elems < (size_t)j0) return -1;
+        transpose_kernel<<<(unsigned)((m + 63) / 64), 256, 0, st>>>(sp, cnt, m, out + j0, ldo,
+                                                                    out_elems - j0, flag);
         if (hipGetLastError() != hipSuccess) return -3;
     }
     return 0;

@@ -427,6 +427,24 @@ __device__ __forceinline__ long long ring_entry(const StreamArgs &a, int W, int 
 // ring_extract_kernel): 4096^2 218 us per load, against 289 us with
 // consecutive lanes of one column (stores and reads scattered) and 249 us
 // with consecutive columns of one row (profiles/r04/ringload).
+// Bounds guard of the flat-pointer ring kernels: an
+// entry outside the tile's Lt entries, or an output index past the caller's
+// buffer, is not accessed; it sets err[5] (kErrBounds), which the host checks
+// after the copy (check_bounds, capi.hip).  One compare per thread.
+constexpr int kErrBounds = 5;
+__device__ __forceinline__ bool ring_ok(const StreamArgs &a, long long e)
+{
+    if (e >= 0 && e < a.Lt) return true;
+    atomicOr(a.err + kErrBounds, 1u);
+    return false;
+}
+__device__ __forceinline__ bool out_ok(const StreamArgs &a, size_t i, size_t n)
+{
+    if (i < n) return true;
+    atomicOr(a.err + kErrBounds, 2u);
+    return false;
+}
+
 __global__ void ring_load_kernel(StreamArgs a, int W, const double *w)
 {
     const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -444,13 +462,14 @@ __global__ void ring_load_kernel(StreamArgs a, int W, const double *w)
         const size_t j = (size_t)row * a.cf.nx + col;
         v = d2{w[j], w[n + j]};
     }
-    a.ring[((size_t)tile * a.Lt + ring_entry(a, W, 0, cl, lane)) * kWave + lane] = v;
+    const long long e = ring_entry(a, W, 0, cl, lane);
+    if (ring_ok(a, e)) a.ring[((size_t)tile * a.Lt + e) * kWave + lane] = v;
 }
 
 // Snapshot extraction: out[e * ldo + j] = element e of state (k0 + j*kstep),
 // e over the 2*nx*ny C-order state (u plane | v plane), j < count.
 __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int count,
-                                    double *out, int ldo)
+                                    double *out, int ldo, size_t out_elems)
 {
     const size_t n = (size_t)a.cf.nx * a.cf.ny;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -461,8 +480,9 @@ __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int 
     const int ti = row / kWave, lane = row - ti * kWave;
     const int tj = col / W, cl = col - tj * W;
     const int tile = ti * a.ntj + tj;
-    const d2 v = a.ring[((size_t)tile * a.Lt + ring_entry(a, W, k0 + j * kstep, cl, lane)) * kWave +
-                        lane];
+    const long long e = ring_entry(a, W, k0 + j * kstep, cl, lane);
+    if (!ring_ok(a, e) || !out_ok(a, (n + cell) * ldo + j, out_elems)) return;
+    const d2 v = a.ring[((size_t)tile * a.Lt + e) * kWave + lane];
     out[cell * ldo + j] = v.x;
     out[(n + cell) * ldo + j] = v.y;
 }
@@ -472,7 +492,7 @@ __global__ void ring_extract_kernel(StreamArgs a, int W, int k0, int kstep, int 
 // Consecutive threads walk j: the reads gather 16-B cells from the ring, the
 // writes are the contiguous rows of the .npy file.
 __global__ void ring_extract_rows_kernel(StreamArgs a, int W, size_t e0, size_t ne, int k0,
-                                         int kstep, int ncols, double *out)
+                                         int kstep, int ncols, double *out, size_t out_elems)
 {
     const size_t n = (size_t)a.cf.nx * a.cf.ny;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -486,8 +506,9 @@ __global__ void ring_extract_rows_kernel(StreamArgs a, int W, size_t e0, size_t 
     const int ti = row / kWave, lane = row - ti * kWave;
     const int tj = col / W, cl = col - tj * W;
     const int tile = ti * a.ntj + tj;
-    const d2 v = a.ring[((size_t)tile * a.Lt + ring_entry(a, W, k0 + j * kstep, cl, lane)) * kWave +
-                        lane];
+    const long long en = ring_entry(a, W, k0 + j * kstep, cl, lane);
+    if (!ring_ok(a, en) || !out_ok(a, idx, out_elems)) return;
+    const d2 v = a.ring[((size_t)tile * a.Lt + en) * kWave + lane];
     out[idx] = vplane ? v.y : v.x;
 }
 
@@ -609,22 +630,22 @@ int launch_ring_load(const StreamArgs &a, int W, const double *w, hipStream_t st
 }
 
 int launch_ring_extract_rows(const StreamArgs &a, int W, size_t e0, size_t ne, int k0, int kstep,
-                             int ncols, double *out, hipStream_t st)
+                             int ncols, double *out, size_t out_elems, hipStream_t st)
 {
     const size_t total = ne * (size_t)ncols;
     if (total == 0) return 0;
     hipLaunchKernelGGL(ring_extract_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       st, a, W, e0, ne, k0, kstep, ncols, out);
+                       st, a, W, e0, ne, k0, kstep, ncols, out, out_elems);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
 int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count, double *out,
-                        int ldo, hipStream_t st)
+                        int ldo, size_t out_elems, hipStream_t st)
 {
     const size_t total = (size_t)a.cf.nx * a.cf.ny * count;
     if (total == 0) return 0;
     hipLaunchKernelGGL(ring_extract_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       st, a, W, k0, kstep, count, out, ldo);
+                       st, a, W, k0, kstep, count, out, ldo, out_elems);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 13
+#define BURG_ABI_VERSION 14
 
 enum burg_status {
     BURG_OK = 0,
@@ -122,6 +122,27 @@ enum burg_engine {
 
 int burg_abi_version(void);
 const char *burg_last_error(void);
+
+/* Source id of this build: the first 16 hex digits of the SHA-256 of the
+ * library's sources (finitedifference_amd/csrc/ *.h, *.hip in byte order, then
+ * its Makefile and this header), fixed at compile time.  finitedifference_amd
+ * ._lib.source_id() computes the same digest from a checkout, so a test run
+ * can show that the shipped binary was built from the tree it runs in. */
+const char *burg_build_id(void);
+
+/* Host-only audit of the pipe engine's trajectory ring (no GPU, no context):
+ * replays, for tile width W, a num_steps trajectory keeping every
+ * snap_every-th state (ring_cap > 0: a working ring of ring_cap W + 128
+ * entries with retained windows, a plain ring of ring_cap steps without), the
+ * ring entries that every kernel touching the ring forms -- the initial-state
+ * load, the compute waves' store walk (RetCursor), the loader wave's read
+ * walk, the snapshot extracts -- and checks them against the ring's entries
+ * per tile and against ring_pos.  report[9]: accesses checked, largest entry,
+ * entries per tile, out-of-range entries, walk/ring_pos mismatches, retained
+ * cells overwritten before the trajectory ended, ring entries overwritten
+ * before the loader read them, retained states, snap_every used.  Returns
+ * BURG_OK when the plan exists (the counts say whether it is sound). */
+int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t *report);
 
 /* Create a context on HIP device `device` for an nx x ny grid (single GPU). */
 int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);

@@ -29,11 +29,28 @@ def orc():
 @pytest.fixture(scope="session")
 def gpu():
     """Skip-free GPU gate: a gpu-marked test fails loudly if the HIP library or
-    the device is missing (no silent fallback)."""
+    the device is missing (no silent fallback), or if the library was not
+    built from the sources in this tree."""
     import torch  # noqa: F401  (device plumbing only; import checks ROCm runtime)
     from finitedifference_amd import _lib
     _lib.load()
+    bid, sid = _lib.build_id(), _lib.source_id()
+    assert bid == sid, (f"libburgers_hip.so build id {bid} != source id {sid} of this checkout: "
+                        "rebuild (make -C finitedifference_amd/csrc)")
     return _lib
+
+
+def pytest_terminal_summary(terminalreporter):
+    """The library's build id next to the checkout's source id, at the end of
+    every run (so a run's tail ties its results to the binary it loaded)."""
+    try:
+        from finitedifference_amd import _lib
+        bid, sid = _lib.build_id(), _lib.source_id()
+    except Exception as e:  # noqa: BLE001  (no library: say so, do not fail the summary)
+        terminalreporter.write_line(f"libburgers_hip build id: unavailable ({e})")
+        return
+    terminalreporter.write_line(f"libburgers_hip build id {bid}, sources {sid}: "
+                                f"{'match' if bid == sid else 'MISMATCH'}")
 
 
 @pytest.fixture(autouse=True)

@@ -152,3 +152,23 @@ def test_n8_slab_keeps_every_10th_state(gpu, orc):
         col = ctx.trajectory_snaps(j, 1)
         assert np.array_equal(col[:, 0], ref[j // 10]), f"state {j * k}"
     ctx.close()
+
+
+def test_set_engine_drops_the_retained_record(gpu):
+    """burg_set_engine frees the ring a trajectory left resident: the record
+    goes with it (BURG_ESTATE), instead of a copy reading a freed ring
+    (ADVICE r04)."""
+    from finitedifference_amd._lib import BURG_ESTATE, BurgersError
+    nx, ny, T = 512, 130, 6
+    ctx = _ctx(nx, ny, engine="pipe", stream_w=64)
+    ctx.upload(np.ones(2 * nx * ny))
+    ctx.trajectory(T, snap_every=2)
+    assert ctx.retained() == (0, T // 2 + 1, 2)
+    ctx.set_engine("pipe", stream_w=128)  # a new plan: the ring is freed
+    with pytest.raises(BurgersError) as ei:
+        ctx.retained()
+    assert ei.value.code == BURG_ESTATE
+    with pytest.raises(BurgersError) as ei:
+        ctx.trajectory_snaps(0, 1)
+    assert ei.value.code == BURG_ESTATE
+    ctx.close()
