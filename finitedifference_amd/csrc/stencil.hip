@@ -173,15 +173,28 @@ __global__ __launch_bounds__(kBlock) void residual_kernel(Coeffs cf, const doubl
     block_sumsq(sq, partials + (size_t)by * nbx + bx);
 }
 
-__global__ __launch_bounds__(kBlock) void sum_partials_kernel(const double *partials, int np,
-                                                              double *out)
+// ||R||^2 from the per-block partials, in a fixed order (deterministic): 1024
+// threads, each summing a strided slice with every load issued up front
+// (independent accumulators), then an LDS tree.  (Round 4's 256-thread loop
+// of dependent loads took 27 us at 8192^2 -- 16 384 partials -- 4.4 % of the
+// residual; profiles/r05/r5base.)
+constexpr int kSumThreads = 1024;
+__global__ __launch_bounds__(kSumThreads) void sum_partials_kernel(const double *partials, int np,
+                                                                   double *out)
 {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < np; i += kBlock) s += partials[i];
-    __shared__ double red[kBlock];
-    red[threadIdx.x] = s;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int i = threadIdx.x;
+    for (; i + 3 * kSumThreads < np; i += 4 * kSumThreads) {
+        a0 += partials[i];
+        a1 += partials[i + kSumThreads];
+        a2 += partials[i + 2 * kSumThreads];
+        a3 += partials[i + 3 * kSumThreads];
+    }
+    for (; i < np; i += kSumThreads) a0 += partials[i];
+    __shared__ double red[kSumThreads];
+    red[threadIdx.x] = (a0 + a1) + (a2 + a3);
     __syncthreads();
-    for (int k = kBlock / 2; k > 0; k >>= 1) {
+    for (int k = kSumThreads / 2; k > 0; k >>= 1) {
         if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
         __syncthreads();
     }
@@ -373,7 +386,7 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
     case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
     default: residual_kernel<true, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
     }
-    if (sumsq) sum_partials_kernel<<<1, kBlock, 0, st>>>(partials, nb, sumsq);
+    if (sumsq) sum_partials_kernel<<<1, kSumThreads, 0, st>>>(partials, nb, sumsq);
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }
 
