@@ -219,6 +219,7 @@ struct PipeArgs {
     int nd, nti_d, ny_d;
     size_t colc_dstride;
     int wg_cm;            // workgroup order: 1 column-major (tile row fastest), 0 row-major
+    int pair;             // W = 16 run kernel with paired 8-column halves (pipe.hip PAIR)
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid
     unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)

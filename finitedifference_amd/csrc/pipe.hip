@@ -62,6 +62,7 @@
 // (err[3] = 64) instead of stalling.  Every later wait is bounded in wall time
 // (s_memrealtime): a wave that gives up sets the error word and the LDS abort
 // flag, and the launch drains.
+#include <algorithm>
 #include <climits>
 #include <cstddef>
 #include <type_traits>
@@ -80,6 +81,7 @@
 
 namespace burg {
 const void *pipe_narrow_fn(int W, bool sweep);  // pipe_narrow.hip
+const void *pipe_pair_fn();                     // pipe_narrow.hip: pipe_kernel<16, false, true>
 namespace {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -395,7 +397,11 @@ struct PipeLds {
 // 6-wave workgroups then no longer fit one CU.
 extern __shared__ __attribute__((aligned(16))) unsigned char pipe_lds_image[];
 
-template <int W, bool SWEEP>
+// PAIR (W = 16 run kernel only): the tile's two
+// 8-column halves A (columns 0-7) and B (8-15) are marched by the same lanes,
+// B one step behind A, so every lane carries two independent cell chains per
+// diagonal -- each diagonal covers two columns, the launch half the diagonals.
+template <int W, bool SWEEP, bool PAIR = false>
 __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 {
     constexpr int kThreads = threads_of<W>();
@@ -530,8 +536,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             for (int c = 0; c < W; ++c) {
                 const long long e = ring_pos(c + lane - W, a.origin, a.L, W, a.ret_k, a.ret_n, a.ret_base);
                 const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
-                sm.st[wave][(c + lane) & (W - 1)][lane] = x0;
-                if constexpr (SWEEP) sm.st0[wave][(c + lane) & (W - 1)][lane] = x0;
+                // (PAIR: half A in slots 0-7, half B in 8-15, slot (c + lane) mod 8)
+                const int slot = PAIR ? ((c & 8) | ((c + lane) & 7)) : ((c + lane) & (W - 1));
+                sm.st[wave][slot][lane] = x0;
+                if constexpr (SWEEP) sm.st0[wave][slot][lane] = x0;
             }
         }
     }
@@ -575,10 +583,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const int pS = lds_ldi(&sm.prog[kq]);
             const int p0 = lds_ldi(&sm.prog[0]);
             const int p3 = lds_ldi(&sm.prog[3]);
-            const bool wS = rS && qs <= pS + kLA;
-            const bool wN = rN && qn + top <= pS + 2 * kLA;
-            const bool wW = rW && qw * W + lane <= p0 + kLA;
-            const bool wE = rE && qe * W + (W - 1) + lane <= p3 + 2 * kLA;
+            // (PAIR: a paired diagonal covers two stream indices; a lane meets
+            // column 0 of step q at paired diagonal 8 q + lane, column 15 at
+            // 8 q + 15 + lane)
+            const bool wS = rS && (PAIR ? qs <= 2 * (pS + kLA) : qs <= pS + kLA);
+            const bool wN = rN && (PAIR ? qn + 2 * top <= 2 * (pS + 2 * kLA) : qn + top <= pS + 2 * kLA);
+            const bool wW = rW && (PAIR ? 8 * qw + lane <= p0 + kLA : qw * W + lane <= p0 + kLA);
+            const bool wE = rE && (PAIR ? 8 * qe + 15 + lane <= p3 + 2 * kLA
+                                        : qe * W + (W - 1) + lane <= p3 + 2 * kLA);
             const int aS = a.qbase + (qs >> LW), aN = a.qbase + (qn >> LW);
             const int aW = a.qbase + qw, aE = a.qbase + qe;
             const int cS = qs & (W - 1), cN = qn & (W - 1);
@@ -820,6 +832,237 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     RetCursor rcur;
     rcur.init(a, W, 0);
     const v4u lempty = lds_empty_g();
+
+    if constexpr (PAIR) {
+        // ============ paired halves ============
+        // Lane r at paired diagonal s: local time tau = s - r; half A works
+        // on column tau mod 8 of step tau / 8, half B on column 8 + tau mod 8
+        // of the step before.  A's west inflow: the tile's west edge at its
+        // column 0, else its own east outflow of the previous diagonal; B's:
+        // A's east outflow of the previous diagonal at column 8 (A's column 7
+        // of the same step), else its own.  South: lane r - 1's north outflow
+        // of the previous diagonal (lane 0: the south inbox, stream index
+        // 16 step + column).  Previous states: LDS slot s mod 8 (A) and 8 +
+        // s mod 8 (B), written 8 paired diagonals earlier.  The ring keeps
+        // the standard W = 16 layout (extraction unchanged): the A cell of
+        // (step q, column c) at diagonal 16 q + c + r, per lane.
+        static_assert(W == 16 && !SWEEP && U == 8, "paired halves: the W = 16 run kernel, blocks of 8");
+        LDS int *const sink = (LDS int *)&sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
+        LDS v4u *const dumpv = &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
+        const int K8 = 8 * K;
+        const int total2 = K8 + 8 + kWave - 1;  // lane 63's B cell ends at local time 8K + 7
+        long long e0l = (long long)a.origin + 16LL * ((-lane) >> 3) + ((-lane) & 7) + lane;
+        e0l %= a.L;
+        if (e0l < 0) e0l += a.L;
+        unsigned eA = (unsigned)e0l;  // ring entry of the lane's A cell (+1 per diagonal, +9 past column 7)
+        double eAx = 0.0, eAy = 0.0, eBx = 0.0, eBy = 0.0;  // east outflows, previous diagonal
+        double nAx = 0.0, nAy = 0.0, nBx = 0.0, nBy = 0.0;  // north outflows, previous diagonal
+        unsigned long long pspins = 0, pslow = 0, pieee = 0, pnonfin = 0, pwait = 0;
+        unsigned pwhy[5] = {0, 0, 0, 0, 0};
+        bool paborted = false;
+        // missing inflows / grants of block [sb, sb + 8): name_it = false: any
+        // (one ballot); true: the kinds (bits as err[3] >> 8)
+        auto missing2 = [&](int sb, bool name_it) -> unsigned {
+            const int t0 = sb - lane, c0 = t0 & 7;
+            const int uw = (8 - c0) & 7, tw = t0 + uw;  // the lane's A column 0 in the block
+            const bool nw = has_west & ((unsigned)tw < (unsigned)K8) & rowok;
+            const v4u gw = lds_ld(&src_w[(tw >> 3) & (kRL - 1)][lane]);
+            const bool miss_w = nw & !l_is_data(gw);
+            const int d = 2 * sb - 8 + lane;  // lanes 0-15: the block's 16 south stream indices
+            const unsigned hs = lds_ld32((const LDS char *)&sm.ins[k][d & (kNI - 1)] + 4);
+            const bool miss_s = has_south & (lane < 16) & (d >= 0) & (d < KW) & (hs == kLdsEmptyHi);
+            const int ue = (7 - c0) & 7, te = t0 + ue, qe = (te >> 3) - 1;  // B column 15 (step qe)
+            const bool oe = ((unsigned)qe < (unsigned)K) & rowok;
+            const unsigned he = lds_ld32((const LDS char *)&sm.ewe[east_lds ? k : 0][qe & (kRL - 1)][lane] + 4);
+            const int pe = lds_ldi(&sm.pe_row[lane]);
+            const bool miss_el = oe & east_lds & (he != kLdsEmptyHi);
+            const bool miss_eg = oe & east_glob & (qe >= pe);
+            const int pn = lds_ldi(&sm.perm[k]);
+            const int tt = min(sb + 7 - top, K8 + 7);  // the top lane's last local time in the block
+            const int th = min(16 * (tt >> 3) + (tt & 7) - (tt >= K8 ? 8 : 0), KW - 1);
+            const bool miss_n = has_north & (tt >= 0) & (th >= pn);
+            if (!name_it)
+                return __builtin_amdgcn_ballot_w64(miss_w | miss_s | miss_el | miss_eg | miss_n) != 0;
+            unsigned why = 0;
+            if (any_lane(miss_w)) why |= 1u;
+            if (any_lane(miss_s)) why |= 2u;
+            if (any_lane(miss_el)) why |= 4u;
+            if (any_lane(miss_eg)) why |= 8u;
+            if (any_lane(miss_n)) why |= 16u;
+            return why;
+        };
+        struct In2 {
+            v4u xa, xb, ca, cb, gw, gsa, gsb;
+        };
+        auto fetch2 = [&](int s) -> In2 {
+            In2 in;
+            const int tau = s - lane;
+            const int cA = tau & 7, qA = tau >> 3;
+            const int sl = s & 7;
+            in.xa = my_st[sl * kWave + lane];
+            in.xb = my_st[(8 + sl) * kWave + lane];
+            in.ca = sm.cc[k][cA];
+            in.cb = sm.cc[k][8 + cA];
+            const bool need_w = has_west & (cA == 0) & ((unsigned)tau < (unsigned)K8) & rowok;
+            in.gw = lds_ld(need_w ? &src_w[qA & (kRL - 1)][lane] : &sm.zero);
+            const int dA0 = 16 * (s >> 3) + (s & 7);  // lane 0's stream indices: A, and B = A - 8
+            in.gsa = lds_ld((has_south & (s < K8)) ? &sm.ins[k][dA0 & (kNI - 1)] : &sm.zero);
+            in.gsb = lds_ld((has_south & (s >= 8) & (s - 8 < K8)) ? &sm.ins[k][(dA0 - 8) & (kNI - 1)] : &sm.zero);
+            return in;
+        };
+        auto mkpre = [&](const v4u xv, const v4u cv, bool inlet) -> MarchCell::Pre {
+            const d2 x = as_d2(xv), co = as_d2(cv);
+            MarchCell::Pre p;
+            const double pu = x.x, pv = x.y;
+            const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
+            const double sl = inlet ? co.y + lb : co.y;
+            p.hx = hx;
+            const double hu = 0.5 * pu;
+            p.xfp = ax * (hu * pu);
+            p.xhp = ax * (hu * pv);
+            p.yhp = ay * (hu * pv);
+            p.ygp = ay * ((0.5 * pv) * pv);
+            p.bu = ((pu - p.xfp) - p.yhp) + sl;
+            p.bv = (pv - p.ygp) - p.xhp;
+            return p;
+        };
+        auto diag2 = [&](const int s, const In2 &in) {
+            const int tau = s - lane;
+            const int cA = tau & 7, qA = tau >> 3, qB = qA - 1;
+            const bool vA = (unsigned)tau < (unsigned)K8;
+            const bool vB = (unsigned)(tau - 8) < (unsigned)K8;
+            const bool at0 = cA == 0, atE = cA == 7;
+            const MarchCell::Pre pa = mkpre(in.xa, in.ca, col0_tile & at0);
+            const MarchCell::Pre pb = mkpre(in.xb, in.cb, false);
+            const MarchCell::Row rw{ay, hy, lb};
+            const d2 g = as_d2(in.gw);
+            const double wa0 = at0 ? g.x : eAx, wa1 = at0 ? g.y : eAy;
+            const double wb0 = at0 ? eAx : eBx, wb1 = at0 ? eAy : eBy;
+            const d2 sa = as_d2(in.gsa), sb2 = as_d2(in.gsb);
+            const double na0 = shr1_or(sa.x, nAx), na1 = shr1_or(sa.y, nAy);
+            const double nb0 = shr1_or(sb2.x, nBx), nb1 = shr1_or(sb2.y, nBy);
+            double oeA0, oeA1, onA0, onA1, oA0, oA1, oeB0, oeB1, onB0, onB1, oB0, oB1;
+            bool okA, okB;
+            MarchCell::chain<true>(pa, rw, wa0, wa1, na0, na1, oeA0, oeA1, onA0, onA1, oA0, oA1, okA);
+            MarchCell::chain<true>(pb, rw, wb0, wb1, nb0, nb1, oeB0, oeB1, onB0, onB1, oB0, oB1, okB);
+            const unsigned long long badA =
+                __builtin_amdgcn_ballot_w64(!okA) & __builtin_amdgcn_ballot_w64(vA) & rowmask;
+            const unsigned long long badB =
+                __builtin_amdgcn_ballot_w64(!okB) & __builtin_amdgcn_ballot_w64(vB) & rowmask;
+            if (__builtin_expect(badA != 0, 0)) {
+                MarchCell::chain<false>(pa, rw, wa0, wa1, na0, na1, oeA0, oeA1, onA0, onA1, oA0, oA1, okA);
+                ++pieee;
+                if (__any(vA && rowok && !(__builtin_isfinite(oA0) && __builtin_isfinite(oA1)))) ++pnonfin;
+            }
+            if (__builtin_expect(badB != 0, 0)) {
+                MarchCell::chain<false>(pb, rw, wb0, wb1, nb0, nb1, oeB0, oeB1, onB0, onB1, oB0, oB1, okB);
+                ++pieee;
+                if (__any(vB && rowok && !(__builtin_isfinite(oB0) && __builtin_isfinite(oB1)))) ++pnonfin;
+            }
+            eAx = oeA0;
+            eAy = oeA1;
+            eBx = oeB0;
+            eBy = oeB1;
+            nAx = onA0;
+            nAy = onA1;
+            nBx = onB0;
+            nBy = onB1;
+            // ---- outputs (a half that has not started keeps its step-0 state)
+            const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
+            const int sl = s & 7;
+            if (tau >= 0) my_st[sl * kWave + lane] = outA;
+            if (tau >= 8) my_st[(8 + sl) * kWave + lane] = outB;
+            const unsigned eB = eA >= 8u ? eA - 8u : eA + Lu - 8u;
+            st_plain(ring, vA ? eA * 1024u + lane16 : kOOB, outA);
+            st_plain(ring, vB ? eB * 1024u + lane16 : kOOB, outB);
+            eA += atE ? 9u : 1u;
+            if (eA >= Lu) eA -= Lu;
+            // east edge: B's column 15 (step qB)
+            const bool out_e = atE & vB & rowok;
+            const v4u eo = as_v4u(oeB0, oeB1);
+            if (east_lds) lds_st(out_e ? &sm.ewe[k][qB & (kRL - 1)][lane] : dumpv, eo);
+            if (east_glob) st_dev(wbox, out_e ? eb + (unsigned)((a.qbase + qB) & (kR - 1)) * (kWave * G) : kOOB, eo);
+            // north edge: the top lane's A (step qA, column cA) and B (qB, 8 + cA)
+            if (has_north) {
+                const bool tl = lane == top;
+                const unsigned offA = (tl & vA & (cA < ncol_real))
+                                          ? nb + (unsigned)((a.qbase + qA) & (kR - 1)) * nstep + (unsigned)cA * ncol
+                                          : kOOB;
+                const unsigned offB = (tl & vB & (8 + cA < ncol_real))
+                                          ? nb + (unsigned)((a.qbase + qB) & (kR - 1)) * nstep + (unsigned)(8 + cA) * ncol
+                                          : kOOB;
+                st_sys(nrs, offA, as_v4u(onA0, onA1));
+                st_sys(nrs, offB, as_v4u(onB0, onB1));
+            }
+            // the consumed west granule back to empty
+            if (has_west) {
+                const bool need_w = at0 & vA & rowok;
+                lds_st(need_w ? &src_w[qA & (kRL - 1)][lane] : dumpv, lempty);
+            }
+        };
+        __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
+        for (int sb = 0; sb < total2; sb += U) {
+            lds_sti(lane == 0 ? &sm.prog[k] : sink, sb);
+            if (__builtin_expect(missing2(sb, false) != 0, 0)) {
+                long long t0 = 0;
+                unsigned long long c0 = 0;
+                bool waited = false;
+                for (;;) {
+                    const unsigned why = missing2(sb, true);
+                    if (!why) break;
+                    if (!waited) {
+                        waited = true;
+                        t0 = now_rt();
+                        c0 = __builtin_amdgcn_s_memtime();
+                        ++pslow;
+                        pwhy[0] += (why & 12u) != 0;
+                        pwhy[1] += (why & 16u) != 0;
+                        pwhy[2] += (why & 1u) != 0;
+                        pwhy[3] += (why & 2u) != 0;
+                    } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
+                        if (lane == 0 && !lds_ldi(&sm.perm[5])) {
+                            lds_sti(&sm.perm[5], 1);
+                            if (atomicOr(a.err, 1u) == 0) {
+                                a.err[1] = (unsigned)tile;
+                                a.err[2] = (unsigned)sb;
+                                a.err[3] = 32u | (why << 8);
+                            }
+                        }
+                        paborted = true;
+                        break;
+                    }
+                    ++pspins;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                if (waited) pwait += __builtin_amdgcn_s_memtime() - c0;
+                if (paborted) break;
+            }
+            In2 cur = fetch2(sb);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                In2 nxt;
+                if (u + 1 < U) nxt = fetch2(sb + u + 1);
+                diag2(sb + u, cur);
+                if (u + 1 < U) cur = nxt;
+            }
+            // the block's south inbox slots back to empty: lane i frees index 2 sb - 8 + i
+            if (has_south) {
+                const int d = 2 * sb - 8 + lane;
+                lds_st(((lane < 16) & (d >= 0) & (d < KW)) ? &sm.ins[k][d & (kNI - 1)] : dumpv, lempty);
+            }
+        }
+        if (lane == 0) {
+            if (pspins) atomicAdd(&a.stats->stall_spins, pspins);
+            if (pslow) atomicAdd(&a.stats->slow_diagonals, pslow);
+            if (pieee) atomicAdd(&a.stats->ieee_diagonals, pieee);
+            if (pnonfin) atomicAdd(&a.stats->nonfinite_diagonals, pnonfin);
+            if (pwait) atomicAdd(&a.stats->slow_ticks, pwait);
+            for (int i = 0; i < 5; ++i)
+                if (pwhy[i]) atomicAdd(&a.stats->why[i], (unsigned long long)pwhy[i]);
+            atomicAdd(&a.stats->tile_steps, (unsigned long long)K);
+        }
+        return;
+    }
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
     unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0, wait_ticks = 0;
@@ -1389,6 +1632,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 #if BURG_PIPE_NARROW_TU
 }  // namespace
 
+const void *pipe_pair_fn() { return (const void *)pipe_kernel<16, false, true>; }
+
 const void *pipe_narrow_fn(int W, bool sweep)
 {
     if (sweep) return W == 8 ? (const void *)pipe_kernel<8, true> : W == 16 ? (const void *)pipe_kernel<16, true> : nullptr;
@@ -1533,6 +1778,13 @@ int pipe_max_resident_blocks(int W, bool sweep)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
         hipSuccess)
         return -3;
+    if (W == 16 && !sweep) {  // the paired-halves build of the same plan must fit as well
+        int np = 0;
+        if (!set_lds_limit(pipe_pair_fn(), dyn) ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, pipe_pair_fn(), 5 * kWave, dyn) != hipSuccess)
+            return -3;
+        n = std::min(n, np);
+    }
     return n * ncu;
 }
 
@@ -1541,7 +1793,8 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     const int blocks = a.nti * a.nwj;
     const bool sweep = a.colc_b != nullptr;
     if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
-    const void *fn = pipe_fn(W, sweep);
+    if (a.pair && (W != 16 || sweep || a.ret_k != 0)) return -1;
+    const void *fn = a.pair ? pipe_pair_fn() : pipe_fn(W, sweep);
     if (!fn) return -1;
     const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return -1;

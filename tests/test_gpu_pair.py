@@ -1,0 +1,85 @@
+"""GPU parity of the paired-halves W = 16 trajectory kernel (pipe.hip PAIR,
+DESIGN.md section 4.1f): the tile's two 8-column halves marched by the same
+lanes, one step apart -- the same cells in the same op order as the one-cell
+kernel, so every state must be bit-identical to the oracle's sequential
+march (orc_march_step, C/hypernet2D.py:72-131's implicit step) and to the
+one-cell build (BURG_PAIR=0).
+
+Most W = 16 tests elsewhere (chunked ring wrap, capped ring, workgroup order,
+1024^2 x 500 steps, the planted IEEE slow path) run the paired kernel too,
+since it is the default for W = 16 trajectories."""
+import os
+
+import numpy as np
+import pytest
+
+from test_gpu_regime import _ctx, _problem, planted_w0
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nx,ny,T", [
+    (16, 64, 5),      # one tile
+    (24, 20, 6),      # one partial tile, one partial strip (ragged B half)
+    (256, 128, 13),   # 2 strips x 16 tiles, 4 workgroups per strip
+    (200, 70, 9),     # partial last tile (columns 192-199: A real, B padding)
+    (520, 130, 7),    # a partial 4-tile workgroup and a 2-row top strip
+    (64, 300, 4),     # tall: 5 strips, one workgroup per strip
+])
+def test_paired_matches_oracle_and_one_cell_kernel(gpu, orc, monkeypatch, nx, ny, T):
+    P = _problem(orc, nx, ny)
+    w0 = planted_w0(nx, ny)
+    ref, _, _ = P.fom(w0, T)
+    got = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("BURG_PAIR", pair)
+        ctx = _ctx(nx, ny, engine="pipe", stream_w=16)
+        snaps, st, _, _ = ctx.run(w0, T)
+        assert st["stream_w"] == 16 and st["nonfinite_diagonals"] == 0
+        for j in range(T + 1):
+            assert np.array_equal(snaps[:, j], ref[j]), f"BURG_PAIR={pair} step {j}"
+        ctx.upload(w0)
+        ctx.trajectory(T)
+        assert np.array_equal(ctx.download(), ref[T]), f"BURG_PAIR={pair} trajectory"
+        got[pair] = st
+        ctx.close()
+    assert got["1"]["ieee_diagonals"] > 0  # the planted values take the IEEE path in both
+
+
+def test_paired_1024_trajectory_rate_and_bits(gpu, orc, monkeypatch):
+    """run_fom.main's unit at 1024^2: both builds bit-equal (final state and
+    every 50th state) and the paired build's launch time reported."""
+    N, T = 1024, 500
+    P = orc.Problem(N)
+    ref = P.march_traj(np.ones(P.m), T, snap_every=50)
+    ms = {}
+    for pair in ("0", "1"):
+        monkeypatch.setenv("BURG_PAIR", pair)
+        ctx = _ctx(N, N)
+        ctx.upload(np.ones(P.m))
+        ctx.trajectory(T)  # warm
+        st = ctx.trajectory(T)
+        assert st["stream_w"] == 16 and st["stream_launches"] == 1
+        ms[pair] = st["loop_ms"]
+        assert np.array_equal(ctx.download(), ref[-1]), f"BURG_PAIR={pair}"
+        snaps = ctx.trajectory_snaps()
+        for j in range(0, T + 1, 50):
+            assert np.array_equal(snaps[:, j], ref[j // 50]), f"BURG_PAIR={pair} step {j}"
+        ctx.close()
+    print(f"\n1024^2 x 500 trajectory: one-cell {ms['0']:.3f} ms, paired {ms['1']:.3f} ms "
+          f"({ms['0'] / ms['1']:.3f}x)")
+
+
+def test_paired_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path):
+    """The paired kernel behind the multi-GPU halo stream: 2 slab processes on
+    one GPU with W = 16 tiles (the top strip's north outflow of both halves
+    goes through the consumer's device ring)."""
+    from test_gpu_parity import _run_slabs
+    N, T, world = 256, 9, 2
+    _run_slabs(tmp_path, N, T, world, SLAB_W="16")
+    from finitedifference_amd.dist import assemble_snaps
+    parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
+    snaps = assemble_snaps(parts, N, N)
+    ref, _, _ = orc.Problem(N).fom(np.ones(2 * N * N), T)
+    for j in range(T + 1):
+        assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
