@@ -620,12 +620,13 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
     }
     // the W = 16 trajectory kernel marches the tile's two 8-column halves in
     // the same lanes (two independent cell chains per diagonal, pipe.hip
-    // PAIR) -- plain rings only (retained windows and
-    // sweeps take the one-cell kernel).  BURG_PAIR=0 turns it off (A/B knob).
+    // PAIR), trajectories and sweeps -- plain rings
+    // only (retained windows take the one-cell kernel).  BURG_PAIR=0 turns it
+    // off (A/B knob).
     {
         const char *e = std::getenv("BURG_PAIR");
         const bool pair_opt = e ? (std::atoi(e) != 0) : true;
-        a.pair = pair_opt && c->sp.W == 16 && a.colc_b == nullptr && a.ret_k == 0;
+        a.pair = pair_opt && c->sp.W == 16 && a.ret_k == 0;
     }
     a.spin_ticks = c->spin_ticks;
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s

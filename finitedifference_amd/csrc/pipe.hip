@@ -81,7 +81,7 @@
 
 namespace burg {
 const void *pipe_narrow_fn(int W, bool sweep);  // pipe_narrow.hip
-const void *pipe_pair_fn();                     // pipe_narrow.hip: pipe_kernel<16, false, true>
+const void *pipe_pair_fn(bool sweep);           // pipe_narrow.hip: pipe_kernel<16, sweep, true>
 namespace {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         // s mod 8 (B), written 8 paired diagonals earlier.  The ring keeps
         // the standard W = 16 layout (extraction unchanged): the A cell of
         // (step q, column c) at diagonal 16 q + c + r, per lane.
-        static_assert(W == 16 && !SWEEP && U == 8, "paired halves: the W = 16 run kernel, blocks of 8");
+        static_assert(W == 16 && U == 8, "paired halves: W = 16, blocks of 8");
         LDS int *const sink = (LDS int *)&sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
         LDS v4u *const dumpv = &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
         const int K8 = 8 * K;
@@ -857,6 +857,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         unsigned eA = (unsigned)e0l;  // ring entry of the lane's A cell (+1 per diagonal, +9 past column 7)
         double eAx = 0.0, eAy = 0.0, eBx = 0.0, eBy = 0.0;  // east outflows, previous diagonal
         double nAx = 0.0, nAy = 0.0, nBx = 0.0, nBy = 0.0;  // north outflows, previous diagonal
+        // sweeps: each half's trajectory (B trails A by one step, so it
+        // switches to the next trajectory 8 diagonals later): inlet terms,
+        // source rows, first step of the next trajectory (its W columns read
+        // the initial state st0)
+        // (B is never at the domain's column 0: no inlet term of its own)
+        double lbA = lb, lbA_next = lb_next;
+        int qnA = qn, qnB = qn, jlA = 0, jlB = 0;
+        lds_f64 *srcA_cur = src_cur, *srcA_nxt = src_nxt, *srcB_cur = src_cur, *srcB_nxt = src_nxt;
         unsigned long long pspins = 0, pslow = 0, pieee = 0, pnonfin = 0, pwait = 0;
         unsigned pwhy[5] = {0, 0, 0, 0, 0};
         bool paborted = false;
@@ -893,14 +901,24 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         };
         struct In2 {
             v4u xa, xb, ca, cb, gw, gsa, gsb;
+            double srca, srcb;  // sweep: the cells' source terms (their trajectory's row)
         };
         auto fetch2 = [&](int s) -> In2 {
             In2 in;
             const int tau = s - lane;
             const int cA = tau & 7, qA = tau >> 3;
             const int sl = s & 7;
-            in.xa = my_st[sl * kWave + lane];
-            in.xb = my_st[(8 + sl) * kWave + lane];
+            if constexpr (SWEEP) {
+                const bool ntA = qA >= qnA, ntB = qA - 1 >= qnB;
+                in.xa = (ntA ? my_st0 : my_st)[sl * kWave + lane];
+                in.xb = (ntB ? my_st0 : my_st)[(8 + sl) * kWave + lane];
+                in.srca = (ntA ? srcA_nxt : srcA_cur)[cA];
+                in.srcb = (ntB ? srcB_nxt : srcB_cur)[8 + cA];
+            } else {
+                in.xa = my_st[sl * kWave + lane];
+                in.xb = my_st[(8 + sl) * kWave + lane];
+                in.srca = in.srcb = 0.0;
+            }
             in.ca = sm.cc[k][cA];
             in.cb = sm.cc[k][8 + cA];
             const bool need_w = has_west & (cA == 0) & ((unsigned)tau < (unsigned)K8) & rowok;
@@ -910,12 +928,12 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             in.gsb = lds_ld((has_south & (s >= 8) & (s - 8 < K8)) ? &sm.ins[k][(dA0 - 8) & (kNI - 1)] : &sm.zero);
             return in;
         };
-        auto mkpre = [&](const v4u xv, const v4u cv, bool inlet) -> MarchCell::Pre {
+        auto mkpre = [&](const v4u xv, const v4u cv, double srcc, bool inlet, double lbu) -> MarchCell::Pre {
             const d2 x = as_d2(xv), co = as_d2(cv);
             MarchCell::Pre p;
             const double pu = x.x, pv = x.y;
             const double hx = co.x, ax = hx + hx;  // exact: hx = 0.5 * (alpha * inv_dx)
-            const double sl = inlet ? co.y + lb : co.y;
+            const double sl = inlet ? srcc + lbu : srcc;
             p.hx = hx;
             const double hu = 0.5 * pu;
             p.xfp = ax * (hu * pu);
@@ -932,9 +950,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const bool vA = (unsigned)tau < (unsigned)K8;
             const bool vB = (unsigned)(tau - 8) < (unsigned)K8;
             const bool at0 = cA == 0, atE = cA == 7;
-            const MarchCell::Pre pa = mkpre(in.xa, in.ca, col0_tile & at0);
-            const MarchCell::Pre pb = mkpre(in.xb, in.cb, false);
-            const MarchCell::Row rw{ay, hy, lb};
+            const bool ntA = SWEEP && qA >= qnA, ntB = SWEEP && qB >= qnB;
+            const double lbuA = ntA ? lbA_next : lbA;
+            const MarchCell::Pre pa = mkpre(in.xa, in.ca, SWEEP ? in.srca : as_d2(in.ca).y, col0_tile & at0, lbuA);
+            const MarchCell::Pre pb = mkpre(in.xb, in.cb, SWEEP ? in.srcb : as_d2(in.cb).y, false, 0.0);
+            const MarchCell::Row rw{ay, hy, lbuA};
             const d2 g = as_d2(in.gw);
             const double wa0 = at0 ? g.x : eAx, wa1 = at0 ? g.y : eAy;
             const double wb0 = at0 ? eAx : eBx, wb1 = at0 ? eAy : eBy;
@@ -999,6 +1019,24 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 const bool need_w = at0 & vA & rowok;
                 lds_st(need_w ? &src_w[qA & (kRL - 1)][lane] : dumpv, lempty);
             }
+            if constexpr (SWEEP) {
+                // a half that finished the first step of its next trajectory switches
+                if (ntA && atE) {
+                    ++jlA;
+                    qnA += a.T;
+                    lbA = lbA_next;
+                    srcA_cur = srcA_nxt;
+                    const int jn = min(jlA + 1, nsw - 1);
+                    lbA_next = sm.lbt[jn][SWEEP ? lane : 0];
+                    srcA_nxt = (lds_f64 *)&sm.srcb[jn][k][0];
+                }
+                if (ntB && atE) {
+                    ++jlB;
+                    qnB += a.T;
+                    srcB_cur = srcB_nxt;
+                    srcB_nxt = (lds_f64 *)&sm.srcb[min(jlB + 1, nsw - 1)][k][0];
+                }
+            }
         };
         __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
         for (int sb = 0; sb < total2; sb += U) {
@@ -1037,13 +1075,23 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 if (waited) pwait += __builtin_amdgcn_s_memtime() - c0;
                 if (paborted) break;
             }
-            In2 cur = fetch2(sb);
+            if constexpr (SWEEP) {
+                // (inputs read after the previous diagonal: a trajectory switch
+                // there decides which state and source row this one reads)
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                In2 nxt;
-                if (u + 1 < U) nxt = fetch2(sb + u + 1);
-                diag2(sb + u, cur);
-                if (u + 1 < U) cur = nxt;
+                for (int u = 0; u < U; ++u) {
+                    const In2 cur = fetch2(sb + u);
+                    diag2(sb + u, cur);
+                }
+            } else {
+                In2 cur = fetch2(sb);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    In2 nxt;
+                    if (u + 1 < U) nxt = fetch2(sb + u + 1);
+                    diag2(sb + u, cur);
+                    if (u + 1 < U) cur = nxt;
+                }
             }
             // the block's south inbox slots back to empty: lane i frees index 2 sb - 8 + i
             if (has_south) {
@@ -1632,7 +1680,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 #if BURG_PIPE_NARROW_TU
 }  // namespace
 
-const void *pipe_pair_fn() { return (const void *)pipe_kernel<16, false, true>; }
+const void *pipe_pair_fn(bool sweep)
+{
+    return sweep ? (const void *)pipe_kernel<16, true, true> : (const void *)pipe_kernel<16, false, true>;
+}
 
 const void *pipe_narrow_fn(int W, bool sweep)
 {
@@ -1778,10 +1829,10 @@ int pipe_max_resident_blocks(int W, bool sweep)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
         hipSuccess)
         return -3;
-    if (W == 16 && !sweep) {  // the paired-halves build of the same plan must fit as well
+    if (W == 16) {  // the paired-halves build of the same plan must fit as well
         int np = 0;
-        if (!set_lds_limit(pipe_pair_fn(), dyn) ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, pipe_pair_fn(), 5 * kWave, dyn) != hipSuccess)
+        if (!set_lds_limit(pipe_pair_fn(sweep), dyn) ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, pipe_pair_fn(sweep), 5 * kWave, dyn) != hipSuccess)
             return -3;
         n = std::min(n, np);
     }
@@ -1793,8 +1844,8 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     const int blocks = a.nti * a.nwj;
     const bool sweep = a.colc_b != nullptr;
     if (sweep && (a.T < 1 || a.K % a.T != 0 || a.K / a.T > kPipeSweepMax)) return -1;
-    if (a.pair && (W != 16 || sweep || a.ret_k != 0)) return -1;
-    const void *fn = a.pair ? pipe_pair_fn() : pipe_fn(W, sweep);
+    if (a.pair && (W != 16 || a.ret_k != 0)) return -1;
+    const void *fn = a.pair ? pipe_pair_fn(sweep) : pipe_fn(W, sweep);
     if (!fn) return -1;
     const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return -1;

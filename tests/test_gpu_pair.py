@@ -83,3 +83,27 @@ def test_paired_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path):
     ref, _, _ = orc.Problem(N).fom(np.ones(2 * N * N), T)
     for j in range(T + 1):
         assert np.array_equal(snaps[:, j], ref[j]), f"step {j}"
+
+
+@pytest.mark.parametrize("nx,ny,nmu,T", [(256, 128, 3, 7), (200, 70, 4, 5), (1024, 1024, 9, 20)])
+def test_paired_sweep_matches_one_cell_and_oracle(gpu, orc, monkeypatch, nx, ny, nmu, T):
+    """burg_sweep on W = 16 tiles with paired halves: every trajectory of the
+    mu sweep (back to back in one launch; B switches trajectory 8 diagonals
+    after A) bit-equal to the oracle's march for its mu and to BURG_PAIR=0."""
+    from finitedifference_amd.config import get_snapshot_params
+    mus = get_snapshot_params()[:nmu]
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("BURG_PAIR", pair)
+        ctx = _ctx(nx, ny, engine="pipe", stream_w=16)
+        ctx.upload(np.ones(2 * nx * ny))
+        snaps, st = ctx.sweep(mus, T)
+        assert st["stream_w"] == 16
+        out[pair] = snaps
+        ctx.close()
+    for j, mu in enumerate(mus):
+        assert np.array_equal(out["1"][j], out["0"][j]), f"mu {j}"
+        if nx <= 256:
+            ref, _, _ = _problem(orc, nx, ny, mu=mu).fom(np.ones(2 * nx * ny), T)
+            for q in range(T + 1):
+                assert np.array_equal(out["1"][j][:, q], ref[q]), f"mu {mu} step {q}"
