@@ -618,14 +618,15 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
         const char *e = std::getenv("BURG_WG_MAP");
         a.wg_cm = e ? (std::atoi(e) != 0) : (c->nwj % 8 == 0);
     }
-    // the W = 16 trajectory kernel marches the tile's two 8-column halves in
-    // the same lanes (two independent cell chains per diagonal, pipe.hip
-    // PAIR), trajectories and sweeps -- plain rings
-    // only (retained windows take the one-cell kernel).  BURG_PAIR=0 turns it
-    // off (A/B knob).
+    // BURG_PAIR=1 (opt-in, round-5 prototype): the W = 16 kernel marches the
+    // tile's two 8-column halves in the same lanes (two independent cell
+    // chains per diagonal, pipe.hip PAIR),
+    // trajectories and sweeps, plain rings only.  Bit-identical, but not
+    // faster: 1024^2 sweep 147 vs 150, trajectory 94 vs 110 Gcell-updates/s
+    // (profiles/r05/ab/pair) -- so it is off by default.
     {
         const char *e = std::getenv("BURG_PAIR");
-        const bool pair_opt = e ? (std::atoi(e) != 0) : true;
+        const bool pair_opt = e ? (std::atoi(e) != 0) : false;
         a.pair = pair_opt && c->sp.W == 16 && a.ret_k == 0;
     }
     a.spin_ticks = c->spin_ticks;

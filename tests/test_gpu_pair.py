@@ -5,9 +5,8 @@ kernel, so every state must be bit-identical to the oracle's sequential
 march (orc_march_step, C/hypernet2D.py:72-131's implicit step) and to the
 one-cell build (BURG_PAIR=0).
 
-Most W = 16 tests elsewhere (chunked ring wrap, capped ring, workgroup order,
-1024^2 x 500 steps, the planted IEEE slow path) run the paired kernel too,
-since it is the default for W = 16 trajectories."""
+The kernel is opt-in (BURG_PAIR=1; measured no faster, profiles/r05/ab/pair):
+these tests select it explicitly."""
 import os
 
 import numpy as np
@@ -76,7 +75,7 @@ def test_paired_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path):
     goes through the consumer's device ring)."""
     from test_gpu_parity import _run_slabs
     N, T, world = 256, 9, 2
-    _run_slabs(tmp_path, N, T, world, SLAB_W="16")
+    _run_slabs(tmp_path, N, T, world, SLAB_W="16", BURG_PAIR="1")
     from finitedifference_amd.dist import assemble_snaps
     parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
     snaps = assemble_snaps(parts, N, N)

@@ -57,8 +57,10 @@ def kind(op):
     return "other"
 
 
-def kernel_body(asm, W, sweep):
-    name = f"_ZN4burg12_GLOBAL__N_111pipe_kernelILi{W}ELb{1 if sweep else 0}EEEvNS_8PipeArgsE:"
+def kernel_body(asm, W, sweep, pair=False):
+    # (round 5: pipe_kernel<W, SWEEP, PAIR>)
+    name = (f"_ZN4burg12_GLOBAL__N_111pipe_kernelILi{W}ELb{1 if sweep else 0}"
+            f"ELb{1 if pair else 0}EEEvNS_8PipeArgsE:")
     i = asm.index(name)
     return asm[i:asm.index(".Lfunc_end", i)].split("\n")
 
@@ -252,11 +254,14 @@ def main():
         asm += open(os.path.join(d, "pipe_narrow-hip-amdgcn-amd-amdhsa-gfx950.s")).read()
     res = {"source": "tools/isa_count.py (hipcc -O3 --offload-arch=gfx950 -save-temps of pipe.hip)",
            "issue_model": "4 cycles per instruction + 12 per fp64 transcendental (one wave per SIMD)"}
-    for W, sweep in ((256, False), (16, True), (16, False)):
+    for W, sweep, pair in ((256, False, False), (16, True, False), (16, False, False),
+                           (16, False, True), (16, True, True)):
         # diagonals per block (pipe.hip: uw_of / BURG_NARROW_U): 16 for wide
-        # tiles of 128 and 256 columns, 8 otherwise (round 3)
-        U = 16 if W in (128, 256) else 8
-        rr = hot_cycle(parse_blocks(kernel_body(asm, W, sweep)), U)
+        # tiles of 128 and 256 columns, 8 otherwise (round 3); the paired
+        # kernel (round 5) runs two cell chains per diagonal: its 8-diagonal
+        # block holds 16 v_rsq_f64, counted here per CELL (x 2 per diagonal)
+        U = 16 if W in (128, 256) or pair else 8
+        rr = hot_cycle(parse_blocks(kernel_body(asm, W, sweep, pair)), U)
         rr = sorted([r for r in rr if len(r) == U], key=lambda r: sum(map(len, r)))
         # wide tiles: steady / interior / edge block variants, shortest first
         # (steady-edge blocks are built twice since round 3: for the
@@ -269,7 +274,7 @@ def main():
                  4: ["steady_block", "interior_block", "steady_edge_block", "edge_block"],
                  5: ["steady_block", "interior_block", "steady_edge_block", "steady_edge_block_east",
                      "edge_block"]}[len(rr)]
-        res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}>"] = {
+        res[f"pipe_kernel<{W}, {'true' if sweep else 'false'}{', paired (per cell)' if pair else ''}>"] = {
             "per_diagonal_averages": {nm: summarise(r) for nm, r in zip(names, rr)}}
     os.makedirs(os.path.dirname(args.out), exist_ok=True)
     with open(args.out, "w") as f:
