@@ -1038,6 +1038,97 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 }
             }
         };
+        // Steady block: a full strip, every lane's A and B inside the
+        // launch for all 8 diagonals, no ring wrap, no trajectory switch.
+        // Every lane then meets A's column 0 exactly once (diagonal uw of the
+        // block; A's column 7 = B's column 15 one before it), so the west
+        // granule is read once, the hand-off targets are fixed per block, the
+        // state slots and south inbox entries sit at constant offsets, and
+        // nothing is masked.
+        auto steady2 = [&](const int sb) {
+            const int t0 = sb - lane, c0 = t0 & 7, q0 = t0 >> 3;
+            const int uw = (8 - c0) & 7;           // A at column 0
+            const int uw8 = c0 == 0 ? 8 : uw;      // A's step advances from here (8: not in this block)
+            const int ue = (uw + 7) & 7;           // A at column 7, B at column 15
+            const int qw = q0 + (c0 == 0 ? 0 : 1);  // A's step at its column 0
+            const int qe = ((t0 + ue) >> 3) - 1;    // B's step at its column 15
+            const v4u gw = lds_ld(has_west ? &src_w[qw & (kRL - 1)][lane] : &sm.zero);
+            LDS v4u *const eaddr = east_lds ? &sm.ewe[k][qe & (kRL - 1)][lane] : dumpv;
+            const unsigned eoff = east_glob ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
+            // ring: A's entry at diagonal u is eA + u (+ 8 from uw8 on); B's is 8 below
+            const unsigned oA1 = eA * 1024u + lane16, oA2 = oA1 + 8192u;
+            // north (top lane): A at (step, column) = (q0, c0 + u) before uw8, (q0 + 1, c0 + u - 8)
+            // after; B one step earlier at column 8 + that
+            const bool tl = has_north & (lane == top);
+            const unsigned sq0 = (unsigned)((a.qbase + q0) & (kR - 1)) * nstep;
+            const unsigned sq1 = (unsigned)((a.qbase + q0 + 1) & (kR - 1)) * nstep;
+            const unsigned sqm = (unsigned)((a.qbase + q0 - 1) & (kR - 1)) * nstep;
+            const unsigned nA1 = tl ? nb + sq0 + (unsigned)c0 * ncol : kOOB;
+            const unsigned nA2 = tl ? nb + sq1 + (unsigned)c0 * ncol - 8u * ncol : kOOB;
+            const unsigned nB1 = tl ? nb + sqm + (unsigned)(8 + c0) * ncol : kOOB;
+            const unsigned nB2 = tl ? nb + sq0 + (unsigned)c0 * ncol : kOOB;
+            const int m16 = 2 * sb;  // lane 0's stream index of A at u = 0 (16 (sb / 8))
+            const LDS v4u *const insA = has_south ? &sm.ins[k][m16 & (kNI - 1)] : &sm.win[0][0][0];
+            const LDS v4u *const insB = has_south ? &sm.ins[k][(m16 - 8) & (kNI - 1)] : &sm.win[0][0][0];
+            const double lbuA = lb;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int ci = (c0 + u) & 7;
+                const bool at0 = u == uw, atE = u == ue;
+                const v4u xa = my_st[u * kWave + lane], xb = my_st[(8 + u) * kWave + lane];
+                const v4u ca = sm.cc[k][ci], cb = sm.cc[k][8 + ci];
+                const v4u gsa = insA[u], gsb = insB[u];
+                double srca = 0.0, srcb = 0.0;
+                if constexpr (SWEEP) {
+                    srca = srcA_cur[ci];
+                    srcb = srcB_cur[8 + ci];
+                }
+                const MarchCell::Pre pa = mkpre(xa, ca, SWEEP ? srca : as_d2(ca).y, col0_tile & at0, lbuA);
+                const MarchCell::Pre pb = mkpre(xb, cb, SWEEP ? srcb : as_d2(cb).y, false, 0.0);
+                const MarchCell::Row rw{ay, hy, lbuA};
+                const d2 g = as_d2(gw);
+                const double wa0 = at0 ? g.x : eAx, wa1 = at0 ? g.y : eAy;
+                const double wb0 = at0 ? eAx : eBx, wb1 = at0 ? eAy : eBy;
+                const d2 sa = as_d2(gsa), sb2 = as_d2(gsb);
+                const double na0 = shr1_or(sa.x, nAx), na1 = shr1_or(sa.y, nAy);
+                const double nb0 = shr1_or(sb2.x, nBx), nb1 = shr1_or(sb2.y, nBy);
+                double oeA0, oeA1, onA0, onA1, oA0, oA1, oeB0, oeB1, onB0, onB1, oB0, oB1;
+                bool okA, okB;
+                MarchCell::chain<true>(pa, rw, wa0, wa1, na0, na1, oeA0, oeA1, onA0, onA1, oA0, oA1, okA);
+                MarchCell::chain<true>(pb, rw, wb0, wb1, nb0, nb1, oeB0, oeB1, onB0, onB1, oB0, oB1, okB);
+                if (__builtin_expect(__builtin_amdgcn_ballot_w64(!(okA & okB)) != 0, 0)) {
+                    // (both halves redone with IEEE sqrt / division: same bits where the fast path held)
+                    MarchCell::chain<false>(pa, rw, wa0, wa1, na0, na1, oeA0, oeA1, onA0, onA1, oA0, oA1, okA);
+                    MarchCell::chain<false>(pb, rw, wb0, wb1, nb0, nb1, oeB0, oeB1, onB0, onB1, oB0, oB1, okB);
+                    pieee += 2;
+                    if (__any(!(__builtin_isfinite(oA0) && __builtin_isfinite(oA1) && __builtin_isfinite(oB0) &&
+                                __builtin_isfinite(oB1))))
+                        ++pnonfin;
+                }
+                eAx = oeA0;
+                eAy = oeA1;
+                eBx = oeB0;
+                eBy = oeB1;
+                nAx = onA0;
+                nAy = onA1;
+                nBx = onB0;
+                nBy = onB1;
+                const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
+                my_st[u * kWave + lane] = outA;
+                my_st[(8 + u) * kWave + lane] = outB;
+                const unsigned oA = (u < uw8 ? oA1 : oA2) + (unsigned)u * 1024u;
+                st_plain(ring, oA, outA);
+                st_plain(ring, oA - 8192u, outB);
+                const v4u eo = as_v4u(oeB0, oeB1);
+                lds_st(atE ? eaddr : dumpv, eo);
+                if (east_glob) st_dev(wbox, atE ? eoff : kOOB, eo);
+                st_sys(nrs, (u < uw8 ? nA1 : nA2) + (unsigned)u * ncol, as_v4u(onA0, onA1));
+                st_sys(nrs, (u < uw8 ? nB1 : nB2) + (unsigned)u * ncol, as_v4u(onB0, onB1));
+            }
+            if (has_west) lds_st(&src_w[qw & (kRL - 1)][lane], lempty);
+            eA += 16u;
+            if (eA >= Lu) eA -= Lu;
+        };
         __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
         for (int sb = 0; sb < total2; sb += U) {
             lds_sti(lane == 0 ? &sm.prog[k] : sink, sb);
@@ -1075,7 +1166,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 if (waited) pwait += __builtin_amdgcn_s_memtime() - c0;
                 if (paborted) break;
             }
-            if constexpr (SWEEP) {
+            bool steady = (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
+                          !any_lane((eA < 8u) | (eA + 15u >= Lu));
+            if constexpr (SWEEP)
+                steady = steady & !any_lane((((sb + U - 1 - lane) >> 3) >= qnA) | ((((sb + U - 1 - lane) >> 3) - 1) >= qnB));
+            if (steady) {
+                steady2(sb);
+            } else if constexpr (SWEEP) {
                 // (inputs read after the previous diagonal: a trajectory switch
                 // there decides which state and source row this one reads)
 #pragma unroll
