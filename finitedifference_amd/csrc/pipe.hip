@@ -1077,7 +1077,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 const bool at0 = u == uw, atE = u == ue;
                 const v4u xa = my_st[u * kWave + lane], xb = my_st[(8 + u) * kWave + lane];
                 const v4u ca = sm.cc[k][ci], cb = sm.cc[k][8 + ci];
-                const v4u gsa = insA[u], gsb = insB[u];
+                // (volatile: the comm wave deposits these -- a plain load could be
+                // hoisted above the readiness wait)
+                const v4u gsa = lds_ld(insA + u), gsb = lds_ld(insB + u);
                 double srca = 0.0, srcb = 0.0;
                 if constexpr (SWEEP) {
                     srca = srcA_cur[ci];
