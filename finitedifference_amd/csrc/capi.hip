@@ -626,8 +626,8 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
     // (profiles/r05/ab/pair) -- so it is off by default.
     {
         const char *e = std::getenv("BURG_PAIR");
-        const bool pair_opt = e ? (std::atoi(e) != 0) : false;
-        a.pair = pair_opt && c->sp.W == 16 && a.ret_k == 0;
+        const int pair_opt = e ? std::atoi(e) : 0;  // (2: without the steady blocks, diagnostics)
+        a.pair = (pair_opt == 1 || pair_opt == 2) && c->sp.W == 16 && a.ret_k == 0 ? pair_opt : 0;
     }
     a.spin_ticks = c->spin_ticks;
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s

@@ -1056,7 +1056,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             LDS v4u *const eaddr = east_lds ? &sm.ewe[k][qe & (kRL - 1)][lane] : dumpv;
             const unsigned eoff = east_glob ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             // ring: A's entry at diagonal u is eA + u (+ 8 from uw8 on); B's is 8 below
-            const unsigned oA1 = eA * 1024u + lane16, oA2 = oA1 + 8192u;
+            // (rA*: byte offsets -- not oA*, the cells' outputs below)
+            const unsigned rA1 = eA * 1024u + lane16, rA2 = rA1 + 8192u;
             // north (top lane): A at (step, column) = (q0, c0 + u) before uw8, (q0 + 1, c0 + u - 8)
             // after; B one step earlier at column 8 + that
             const bool tl = has_north & (lane == top);
@@ -1118,9 +1119,9 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
                 my_st[u * kWave + lane] = outA;
                 my_st[(8 + u) * kWave + lane] = outB;
-                const unsigned oA = (u < uw8 ? oA1 : oA2) + (unsigned)u * 1024u;
-                st_plain(ring, oA, outA);
-                st_plain(ring, oA - 8192u, outB);
+                const unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u;
+                st_plain(ring, rA, outA);
+                st_plain(ring, rA - 8192u, outB);
                 const v4u eo = as_v4u(oeB0, oeB1);
                 lds_st(atE ? eaddr : dumpv, eo);
                 if (east_glob) st_dev(wbox, atE ? eoff : kOOB, eo);
@@ -1168,7 +1169,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 if (waited) pwait += __builtin_amdgcn_s_memtime() - c0;
                 if (paborted) break;
             }
-            bool steady = (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
+            bool steady = (a.pair == 1) & (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
                           !any_lane((eA < 8u) | (eA + 15u >= Lu));
             if constexpr (SWEEP)
                 steady = steady & !any_lane((((sb + U - 1 - lane) >> 3) >= qnA) | ((((sb + U - 1 - lane) >> 3) - 1) >= qnB));
