@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             const int m16 = 2 * sb;  // lane 0's stream index of A at u = 0 (16 (sb / 8))
             const LDS v4u *const insA = has_south ? &sm.ins[k][m16 & (kNI - 1)] : &sm.win[0][0][0];
             const LDS v4u *const insB = has_south ? &sm.ins[k][(m16 - 8) & (kNI - 1)] : &sm.win[0][0][0];
-            const double lbuA = lb;
+            const double lbuA = SWEEP ? lbA : lb;  // (sweep: the lane's current trajectory's inlet term)
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int ci = (c0 + u) & 7;
