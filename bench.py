@@ -108,7 +108,7 @@ def parse():
                          "for the host-side collectives (use small slabs so all ranks' "
                          "workgroups are resident together)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--isa-file", default=os.path.join(ROOT, "profiles", "r03", "pipe_isa.json"))
+    ap.add_argument("--isa-file", default=os.path.join(ROOT, "profiles", "r05", "pipe_isa.json"))
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end field (1024^2 x 500 trajectory + .npy file)")
     return ap.parse_args()
@@ -749,10 +749,19 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
     ms = kern / steps
     gbs = BYTES_PER_CELL_UPDATE * upd / (ms * 1e-3) / 1e9
     traffic, tsrc = read_pmc(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
-    kname = f"pipe_kernel<{st['stream_w']}, true>"
+    paired = st.get("paired_launches", 0) > 0
     clk, csrc = read_clock(pmc_file, f"pipe:{nx}x{nx}:T{T}x9")
-    iss = issue_roofline(kname, ms, T * len(mus) * st["stream_w"] + 2 * nx, isa_file,
-                         st["stream_w"], U=block_of(st["stream_w"]), clock_ghz=clk,
+    if paired:
+        # the paired-halves kernel: two cells per lane
+        # and diagonal, T * nmu * 8 + 2 nx paired diagonals; the ISA counts
+        # and the issue bound are per CELL, so the measured side is too
+        kname = f"pipe_kernel<{st['stream_w']}, true, paired (per cell)>"
+        cell_diags = 2 * (T * len(mus) * st["stream_w"] // 2 + 2 * nx)
+    else:
+        kname = f"pipe_kernel<{st['stream_w']}, true>"
+        cell_diags = T * len(mus) * st["stream_w"] + 2 * nx
+    iss = issue_roofline(kname, ms, cell_diags, isa_file, st["stream_w"],
+                         U=block_of(st["stream_w"]), clock_ghz=clk,
                          clock_src=csrc) if isa_file else None
     # the narrow tiles keep the previous state in LDS: the bytes they move
     # (PMC) are ~0.6 x the 32-B model's, so the fraction on measured traffic
@@ -768,7 +777,8 @@ def config2_1024(pmc_file, isa_file=None, steps=3):
             "roofline_frac_note": "roofline_frac: 32 B per cell-update (SURVEY 8(d)) / kernel "
                                   "time / 8 TB/s; _measured_traffic: PMC HBM bytes per launch "
                                   "(traffic) / kernel time / 8 TB/s",
-            "ieee_diagonals": st["ieee_diagonals"], "traffic": traffic, "traffic_source": tsrc}
+            "ieee_diagonals": st["ieee_diagonals"], "paired_halves": paired,
+            "traffic": traffic, "traffic_source": tsrc}
 
 
 if __name__ == "__main__":

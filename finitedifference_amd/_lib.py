@@ -62,6 +62,7 @@ class BurgStats(ctypes.Structure):
         ("ieee_diagonals", ctypes.c_int64),
         ("comm_polls", ctypes.c_int64),
         ("nonfinite_diagonals", ctypes.c_int64),
+        ("paired_launches", ctypes.c_int64),
     ]
 
     def as_dict(self):

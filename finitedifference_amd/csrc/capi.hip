@@ -183,6 +183,7 @@ struct burg_ctx {
     bool halo_connected = false;
     bool slab_failed = false;        // a launch failed: refuse further launches (BURG_ESTATE)
     int64_t launches = 0;            // march launches of this context (test hook)
+    int64_t paired_launches = 0;     // since stream_stats_begin: launches of the paired kernel
     // side-by-side domains (an internal sweep context, burg_sweep): bat_nd
     // domains of bat_ny_d rows, each padded to whole strips; per-domain column
     // tables bat_colc_stride apart (ov_colc)
@@ -618,15 +619,20 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
         const char *e = std::getenv("BURG_WG_MAP");
         a.wg_cm = e ? (std::atoi(e) != 0) : (c->nwj % 8 == 0);
     }
-    // BURG_PAIR=1 (opt-in, round-5 prototype): the W = 16 kernel marches the
-    // tile's two 8-column halves in the same lanes (two independent cell
-    // chains per diagonal, pipe.hip PAIR),
-    // trajectories and sweeps, plain rings only.  Bit-identical, but not
-    // faster: 1024^2 sweep 147 vs 150, trajectory 94 vs 110 Gcell-updates/s
-    // (profiles/r05/ab/pair) -- so it is off by default.
+    // Paired halves (pipe.hip PAIR): the W = 16 kernel
+    // marches the tile's two 8-column halves in the same lanes, one step
+    // apart -- the per-diagonal control is shared by two cells (97.8 instead
+    // of 108 instructions per cell), but a launch has half the diagonals for
+    // the same pipeline fill (nx + ny diagonals).  So: on for sweeps (the
+    // 1024^2 9-mu sweep 149 -> 172 Gcell-updates/s) and for trajectories
+    // long enough to amortise the fill (K >= (nx + rows) / 2; the 1024^2 x
+    // 500 trajectory stays one-cell: 110 vs 104, profiles/r05/ab/pair).
+    // Plain rings only.  BURG_PAIR=0 / 1 forces it off / on (2: on without
+    // its steady blocks, diagnostics).
     {
         const char *e = std::getenv("BURG_PAIR");
-        const int pair_opt = e ? std::atoi(e) : 0;  // (2: without the steady blocks, diagnostics)
+        int pair_opt = e ? std::atoi(e) : -1;
+        if (pair_opt < 0) pair_opt = (a.T < K || 2LL * K >= (long long)c->nx + c->nrows) ? 1 : 0;
         a.pair = (pair_opt == 1 || pair_opt == 2) && c->sp.W == 16 && a.ret_k == 0 ? pair_opt : 0;
     }
     a.spin_ticks = c->spin_ticks;
@@ -682,7 +688,9 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
     } guard{c};
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
-        CHK(launch_pipe(pipe_args(c, L, origin, K, mp), c->sp.W, c->stream));
+        const PipeArgs pa = pipe_args(c, L, origin, K, mp);
+        CHK(launch_pipe(pa, c->sp.W, c->stream));
+        if (pa.pair) ++c->paired_launches;
     } else {
         if (mp && mp->k > 0) return fail(BURG_EINVAL, "retained windows need the pipe engine");
         CHK(launch_stream(stream_args(c, L, origin, K), c->sp.W, c->stream));
@@ -732,6 +740,7 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
 
 void stream_stats_begin(burg_ctx *c)
 {
+    c->paired_launches = 0;
     (void)hipMemsetAsync(c->d_sstats, 0, sizeof(StreamStats), c->stream);
 }
 
@@ -776,6 +785,7 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->ieee_diagonals = (int64_t)ss.ieee_diagonals;
         st->comm_polls = c->eng_eff == BURG_ENGINE_PIPE ? (int64_t)ss.why[5] : 0;
         st->nonfinite_diagonals = (int64_t)ss.nonfinite_diagonals;
+        st->paired_launches = c->paired_launches;
     }
     if (ss.nonfinite_diagonals && !std::getenv("BURG_ALLOW_NONFINITE"))  // (diagnostics knob)
         return fail(BURG_ENAN,

@@ -107,6 +107,8 @@ typedef struct burg_stats {
     int64_t comm_polls;         /* pipe engine: comm-wave polling rounds (all workgroups) */
     int64_t nonfinite_diagonals; /* stream/pipe: diagonals whose new state held a NaN/Inf
                                     (the call then returns BURG_ENAN) */
+    int64_t paired_launches;    /* pipe engine: launches that ran the paired-halves W = 16
+                                   kernel (two cells per lane and diagonal) */
 } burg_stats;
 
 enum burg_engine {

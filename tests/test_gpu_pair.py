@@ -35,6 +35,7 @@ def test_paired_matches_oracle_and_one_cell_kernel(gpu, orc, monkeypatch, nx, ny
         ctx = _ctx(nx, ny, engine="pipe", stream_w=16)
         snaps, st, _, _ = ctx.run(w0, T)
         assert st["stream_w"] == 16 and st["nonfinite_diagonals"] == 0
+        assert (st["paired_launches"] > 0) == (pair == "1")
         for j in range(T + 1):
             assert np.array_equal(snaps[:, j], ref[j]), f"BURG_PAIR={pair} step {j}"
         ctx.upload(w0)
@@ -98,6 +99,7 @@ def test_paired_sweep_matches_one_cell_and_oracle(gpu, orc, monkeypatch, nx, ny,
         ctx.upload(np.ones(2 * nx * ny))
         snaps, st = ctx.sweep(mus, T)
         assert st["stream_w"] == 16
+        assert (st["paired_launches"] > 0) == (pair == "1")
         out[pair] = snaps
         ctx.close()
     for j, mu in enumerate(mus):
