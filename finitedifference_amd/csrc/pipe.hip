@@ -157,11 +157,17 @@ constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
 #ifndef BURG_WIDE_U16_512
 #define BURG_WIDE_U16_512 1
 #endif
+// BURG_W512_U8 (A/B build, round 5): W = 512 with blocks of 8 in the same
+// 32-diagonal window (the loader then runs up to 3 blocks ahead instead of
+// 1) and the rolling column table
+#ifndef BURG_W512_U8
+#define BURG_W512_U8 0
+#endif
 template <int W>
 constexpr bool u16_of()
 {
     return BURG_WIDE_U16 && !two_per_cu<W>() &&
-           (W == 128 || W == 256 || (BURG_WIDE_U16_512 && (W == 512 || W == 1024)));
+           (W == 128 || W == 256 || (BURG_WIDE_U16_512 && ((W == 512 && !BURG_W512_U8) || W == 1024)));
 }
 // Rolling column table (W >= 512 with blocks of 16): slot t mod kCCW holds
 // {hx, src} of local time t's column while lanes can need it.  A block at
@@ -170,11 +176,11 @@ constexpr bool u16_of()
 // wave's block): 95 < kCCW apart, so no live slot is overwritten.
 constexpr int kCCW = 128;
 template <int W>
-constexpr bool ccw_of() { return u16_of<W>() && W >= 512; }
+constexpr bool ccw_of() { return (u16_of<W>() || (BURG_W512_U8 && W == 512)) && W >= 512; }
 template <int W>
 constexpr int ccn_of() { return ccw_of<W>() ? kCCW : W; }  // column-table slots (before padding)
 template <int W>
-constexpr int win_of() { return two_per_cu<W>() ? 12 : u16_of<W>() ? 32 : W >= 1024 ? 16 : BURG_KWIN; }  // window (diagonals)
+constexpr int win_of() { return two_per_cu<W>() ? 12 : (u16_of<W>() || (BURG_W512_U8 && W == 512)) ? 32 : W >= 1024 ? 16 : BURG_KWIN; }  // window (diagonals)
 template <int W>
 constexpr int uw_of() { return two_per_cu<W>() ? 4 : u16_of<W>() ? 16 : 8; }  // block (diagonals)
 // (blocks of 16: 32 diagonals; BURG_U16_LA for A/B builds)

@@ -5,8 +5,9 @@ kernel, so every state must be bit-identical to the oracle's sequential
 march (orc_march_step, C/hypernet2D.py:72-131's implicit step) and to the
 one-cell build (BURG_PAIR=0).
 
-The kernel is opt-in (BURG_PAIR=1; measured no faster, profiles/r05/ab/pair):
-these tests select it explicitly."""
+The kernel is the default for W = 16 sweeps and long trajectories
+(profiles/r05/ab/pair: 1024^2 9-mu sweep 149 -> 172 Gcell/s); these tests
+select each build explicitly with BURG_PAIR=1 / 0."""
 import os
 
 import numpy as np
