@@ -213,7 +213,7 @@ def end_to_end(nx=1024, T=500):
     """C/run_fom.py:41-43's timed region on the GPU: one {nx}^2 x {T}
     trajectory from w0 = 1 (dt = 0.05, mu = (5.19, 0.026)) including the
     snapshot matrix's device-to-host copy and its .npy file (burg_run_npy:
-    pinned double-buffered writer), wall clock of the call; the file goes to
+    pinned buffers, pwrite writer thread, no fsync as np.save), wall clock of the call; the file goes to
     a temporary directory and is deleted."""
     import tempfile
     from finitedifference_amd.solver import FOMContext

@@ -2737,10 +2737,16 @@ static std::string npy_header(size_t m, size_t ncols)
 }
 
 // burg_run_npy: one trajectory, its snapshot matrix written straight into a
-// .npy file (load_or_compute_snaps' cache, C/hypernet2D.py:3141-3143).  The
-// trajectory stays in the HBM ring; row blocks of the C-order matrix are
-// gathered on the device, copied into one of two pinned host buffers and
-// written by a writer thread while the next block is gathered and copied.
+// .npy file (load_or_compute_snaps' cache, C/hypernet2D.py:3141-3143; np.save
+// in run_fom.main's timed region, C/run_fom.py:41-43).  The trajectory stays
+// in the HBM ring; row blocks of the C-order matrix are gathered on the
+// device, copied into a pool of pinned host buffers and written at their file
+// offsets (pwrite) by writer threads while the next blocks are gathered and
+// copied.  One writer by default: buffered writes into one file serialise on
+// the file (the GPU box's host: 11 GB/s with 1 thread, 10-11 with 2-8;
+// memcpy into a shared mapping 3-7 GB/s; profiles/r05/ab/npy), so the call
+// runs at that rate.  Like np.save, the file is left in the page cache (no
+// fsync; BURG_NPY_FSYNC=1 adds one -- 0.75 -> 1.35 s at 1024^2 x 500).
 int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, const char *path,
                  burg_stats *st)
 {
@@ -2765,29 +2771,46 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         return fail(BURG_ENOMEM, "the %d-step trajectory (%.1f GB of ring) does not fit in HBM; "
                     "use burg_run", num_steps, (double)need / 1e9);
     if (int e = ensure_ring(c, L)) return e;
-    // row blocks: about 128 MB each (at least one row)
+    // row blocks: about 32 MB each (at least one row); NW writer threads
+    // (BURG_NPY_WRITERS, default 1), max(4, 2 NW) pinned buffers
     const size_t row_bytes = (size_t)ncols * sizeof(double);
-    size_t R = std::max<size_t>(1, ((size_t)128 << 20) / row_bytes);
+    size_t R = std::max<size_t>(1, ((size_t)32 << 20) / row_bytes);
     if (const char *e = std::getenv("BURG_NPY_BLOCK_ROWS")) {  // test knob: force many blocks
         const long long v = std::atoll(e);
         if (v > 0) R = std::min(R, (size_t)v);
     }
     R = std::min(R, m);
-    double *d_blk = nullptr, *h_blk[2] = {nullptr, nullptr};
+    int NW = 1;
+    if (const char *e = std::getenv("BURG_NPY_WRITERS")) NW = std::max(1, std::min(16, std::atoi(e)));
+    const int NBUF = std::max(4, 2 * NW);
+    const bool want_fsync = [] {
+        const char *e = std::getenv("BURG_NPY_FSYNC");
+        return e && std::atoi(e) != 0;
+    }();
+    double *d_blk = nullptr;
+    std::vector<double *> h_blk(NBUF, nullptr);
     int fd = -1;
     int rc = BURG_OK;
-    std::thread writer;
+    std::vector<std::thread> writers;
     std::mutex mu;
     std::condition_variable cv;
-    size_t ready_bytes[2] = {0, 0};  // > 0: buffer i holds bytes for the writer
-    bool busy[2] = {false, false}, stop = false, werr = false;
+    struct Job {
+        int buf;
+        off_t off;
+        size_t bytes;
+    };
+    std::vector<Job> jobs;     // filled buffers waiting for a writer
+    std::vector<int> free_buf;  // buffers the device may copy into
+    bool stop = false, werr = false;
+    int werrno = 0;
     auto cleanup = [&]() {
         {
             std::lock_guard<std::mutex> g(mu);
             stop = true;
         }
         cv.notify_all();
-        if (writer.joinable()) writer.join();
+        for (auto &t : writers)
+            if (t.joinable()) t.join();
         (void)hipStreamSynchronize(c->stream);
         dfree(d_blk);
         for (auto &h : h_blk)
@@ -2795,11 +2818,13 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         if (fd >= 0) close(fd);
     };
     if ((rc = dalloc(&d_blk, 2 * R * (size_t)ncols))) return rc;
-    for (auto &h : h_blk)
-        if (hipHostMalloc((void **)&h, R * row_bytes, hipHostMallocDefault) != hipSuccess) {
+    for (int i = 0; i < NBUF; ++i) {
+        if (hipHostMalloc((void **)&h_blk[i], R * row_bytes, hipHostMallocDefault) != hipSuccess) {
             cleanup();
-            return fail(BURG_ENOMEM, "pinned staging buffers (2 x %zu bytes)", R * row_bytes);
+            return fail(BURG_ENOMEM, "pinned staging buffers (%d x %zu bytes)", NBUF, R * row_bytes);
         }
+        free_buf.push_back(i);
+    }
     fd = open(path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
     if (fd < 0) {
         cleanup();
@@ -2810,37 +2835,41 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         cleanup();
         return fail(BURG_EINVAL, "write(%s): %s", path, strerror(errno));
     }
-    writer = std::thread([&]() {
-        int i = 0;
-        for (;;) {
-            size_t nbytes = 0;
-            {
-                std::unique_lock<std::mutex> g(mu);
-                cv.wait(g, [&] { return ready_bytes[i] > 0 || stop; });
-                if (ready_bytes[i] == 0) return;
-                nbytes = ready_bytes[i];
-            }
-            const char *p = (const char *)h_blk[i];
-            size_t left = nbytes;
-            while (left > 0) {
-                const ssize_t wr = write(fd, p, left);
-                if (wr <= 0) {
-                    std::lock_guard<std::mutex> g(mu);
-                    werr = true;
-                    break;
+    for (int w = 0; w < NW; ++w)
+        writers.emplace_back([&]() {
+            for (;;) {
+                Job j;
+                {
+                    std::unique_lock<std::mutex> g(mu);
+                    cv.wait(g, [&] { return !jobs.empty() || stop; });
+                    if (jobs.empty()) return;
+                    j = jobs.back();
+                    jobs.pop_back();
                 }
-                p += wr;
-                left -= (size_t)wr;
+                const char *p = (const char *)h_blk[j.buf];
+                size_t left = j.bytes;
+                off_t off = j.off;
+                bool ok = true;
+                int en = 0;
+                while (left > 0) {
+                    const ssize_t wr = pwrite(fd, p, left, off);
+                    if (wr <= 0) {
+                        ok = false;
+                        en = errno;
+                        break;
+                    }
+                    p += wr;
+                    off += wr;
+                    left -= (size_t)wr;
+                }
+                {
+                    std::lock_guard<std::mutex> g(mu);
+                    if (!ok && !werr) werr = true, werrno = en;
+                    free_buf.push_back(j.buf);
+                }
+                cv.notify_all();
             }
-            {
-                std::lock_guard<std::mutex> g(mu);
-                ready_bytes[i] = 0;
-                busy[i] = false;
-            }
-            cv.notify_all();
-            i ^= 1;
-        }
-    });
+        });
 
     // the trajectory: one launch, every state in the ring
     const auto t_start = std::chrono::steady_clock::now();
@@ -2852,25 +2881,27 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         cleanup();
         return rc;
     }
-    // row blocks -> pinned buffers -> file, double-buffered
+    // row blocks -> pinned buffers -> writer pool -> file
     float flush_ms = 0.f;
     hipEvent_t f0 = nullptr, f1 = nullptr;
     (void)hipEventCreate(&f0);
     (void)hipEventCreate(&f1);
-    int bi = 0;
-    for (size_t e0 = 0; e0 < m && rc == BURG_OK; e0 += R, bi ^= 1) {
+    int di = 0;  // device gather buffer (two, alternating)
+    for (size_t e0 = 0; e0 < m && rc == BURG_OK; e0 += R, di ^= 1) {
         const size_t ne = std::min(R, m - e0);
+        int b = -1;
         {
             std::unique_lock<std::mutex> g(mu);
-            cv.wait(g, [&] { return !busy[bi] || werr; });
+            cv.wait(g, [&] { return !free_buf.empty() || werr; });
             if (werr) break;
-            busy[bi] = true;
+            b = free_buf.back();
+            free_buf.pop_back();
         }
-        double *dst = d_blk + (size_t)bi * R * ncols;
+        double *dst = d_blk + (size_t)di * R * ncols;
         (void)hipEventRecord(f0, c->stream);
         if (launch_ring_extract_rows(stream_args(c, L, 0, 0), W, e0, ne, 0, snap_every, (int)ncols,
                                      dst, R * (size_t)ncols, c->stream) ||
-            hipMemcpyAsync(h_blk[bi], dst, ne * row_bytes, hipMemcpyDeviceToHost, c->stream) !=
+            hipMemcpyAsync(h_blk[b], dst, ne * row_bytes, hipMemcpyDeviceToHost, c->stream) !=
                 hipSuccess) {
             rc = fail(BURG_EHIP, "snapshot row block copy failed");
             break;
@@ -2885,19 +2916,17 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         flush_ms += t;
         {
             std::lock_guard<std::mutex> g(mu);
-            ready_bytes[bi] = ne * row_bytes;
+            jobs.push_back({b, (off_t)(hdr.size() + e0 * row_bytes), ne * row_bytes});
         }
         cv.notify_all();
     }
-    // drain the writer, then stop it
+    // drain the writers
     {
         std::unique_lock<std::mutex> g(mu);
-        cv.wait(g, [&] { return (!busy[0] && !busy[1]) || werr; });
+        cv.wait(g, [&] { return (int)free_buf.size() == NBUF || (werr && jobs.empty()); });
     }
-    if (werr && rc == BURG_OK) rc = fail(BURG_EINVAL, "write(%s) failed", path);
-    if (rc == BURG_OK && fsync(fd) != 0) {
-        // page cache is enough for np.load; fsync failures (e.g. pipes) are not fatal
-    }
+    if (werr && rc == BURG_OK) rc = fail(BURG_EINVAL, "write(%s) failed: %s", path, strerror(werrno));
+    if (rc == BURG_OK && want_fsync) (void)fsync(fd);  // (not fatal: page cache is enough for np.load)
     const double wall_ms =
         std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     if (rc == BURG_OK) {

@@ -181,7 +181,7 @@ class FOMContext:
 
     def run_to_npy(self, w0, num_steps, path, snap_every=1):
         """One trajectory written straight into the .npy file `path`
-        (burg_run_npy: pinned double-buffered writer); returns stats
+        (burg_run_npy: pinned buffers, pwrite writer thread); returns stats
         (loop_ms launch, flush_ms gathers + D2H, march_kernel_ms whole call)."""
         w0 = self._vec(w0, "w0")
         st = _lib.BurgStats()

@@ -1153,9 +1153,11 @@ def test_snapshot_cache_snap_every_and_short_files(gpu, tmp_path):
 
 def test_direct_npy_writer(gpu, tmp_path, monkeypatch):
     """burg_run_npy (load_or_compute_snaps(direct=True)): the file the
-    library writes through its pinned double-buffered writer is np.save's
+    library writes through its pinned buffers and writer pool (pwrite at
+    each row block's offset, blocks finishing out of order) is np.save's
     .npy of the reference's snapshot matrix, byte-identical to np.save of
-    burg_run's matrix; snap_every and multi-block files included."""
+    burg_run's matrix; snap_every, multi-block files and 1 / 3 / 8 writers
+    included."""
     from finitedifference_amd import hypernet2D as H
     N, T = 300, 9
     gx, gy = H.make_2D_grid(0, 100, 0, 100, N, N)
@@ -1172,3 +1174,8 @@ def test_direct_npy_writer(gpu, tmp_path, monkeypatch):
     st = ctx.run_to_npy(w0, T, str(tmp_path / "thin.npy"), snap_every=4)
     assert np.array_equal(np.load(tmp_path / "thin.npy"), ref[:, ::4])
     assert st["loop_ms"] > 0 and st["flush_ms"] > 0
+    monkeypatch.setenv("BURG_NPY_BLOCK_ROWS", "997")  # 181 blocks
+    for nw in ("1", "3", "8"):
+        monkeypatch.setenv("BURG_NPY_WRITERS", nw)
+        ctx.run_to_npy(w0, T, str(tmp_path / f"w{nw}.npy"))
+        assert open(tmp_path / f"w{nw}.npy", "rb").read() == open(tmp_path / "ref.npy", "rb").read(), nw
