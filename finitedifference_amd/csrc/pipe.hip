@@ -94,8 +94,16 @@ constexpr unsigned kLdsEmptyHi = 0x7FF6DEADu;  // LDS slot empty
 constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, stores dropped
 constexpr int kR = kPipeR;
 constexpr unsigned G = kPipeGranuleStride;
-template <int W>
-constexpr int threads_of() { return W > 16 ? 6 * kWave : 5 * kWave; }  // + loader wave
+// BURG_LOADERS: loader waves per wide workgroup.  2 (round 5) = wave 5 fills
+// compute waves 0-1's windows, wave 6 those of waves 2-3: twice the ring DMAs
+// in flight per workgroup (one wave keeps at most 63 loads outstanding, and
+// waits for a round to land before it issues the next); blocks waiting for
+// their window 8.4 M -> 0.2 M per 16384 x 2048 launch, 179 -> 184.5 and
+// 4096^2 184.7 -> 188.7 Gcell-updates/s (profiles/r05/ab/loaders).  1 = the
+// single loader of rounds 2-4.
+#ifndef BURG_LOADERS
+#define BURG_LOADERS 2
+#endif
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
 #ifndef BURG_KLA
 #define BURG_KLA 16
@@ -143,6 +151,11 @@ constexpr int la_of();
 #endif
 template <int W>
 constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
+// loader waves (BURG_LOADERS; at most 2 where two workgroups share a CU)
+template <int W>
+constexpr int nl_of() { return two_per_cu<W>() ? (BURG_LOADERS < 2 ? BURG_LOADERS : 2) : BURG_LOADERS; }
+template <int W>
+constexpr int threads_of() { return W > 16 ? (5 + nl_of<W>()) * kWave : 5 * kWave; }  // + loader wave(s)
 // Blocks of 16 diagonals for W = 128 ... 1024 (round 3 for 128, 256; window
 // 32 diagonals, LDS rings of 2 steps between the workgroup's waves -- the
 // room for it; the LDS DMA reaches past 64 KB, tools/probes/
@@ -677,7 +690,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if (lane == 0) atomicAdd(&a.stats->why[5], iters);
         return;
     }
-    if (WIDE && wave == 5) {
+    if (WIDE && wave >= 5) {
+        const int lw = wave - 5;
         // ================= loader wave (wide tiles) =================
         // window slot d mod KWIN of compute wave k <- ring entry (origin +
         // d - W) of its tile, once (1) the slot's previous diagonal is done
@@ -706,6 +720,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k >= nval) continue;
+                if ((k * nl_of<W>()) >> 2 != lw) continue;  // (this loader's compute waves)
                 const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
                 const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
                 if (nf[k] < lim) {
@@ -1904,6 +1919,21 @@ bool pipe_width_supported(int W) { return pipe_fn(W, false) != nullptr; }
 
 // diagonals per block of the trajectory kernel (its ring walk advances per
 // block; burg_ring_audit replays it)
+static int pipe_threads(int W)
+{
+    switch (W) {
+    case 8: return threads_of<8>();
+    case 16: return threads_of<16>();
+    case 32: return threads_of<32>();
+    case 64: return threads_of<64>();
+    case 128: return threads_of<128>();
+    case 256: return threads_of<256>();
+    case 512: return threads_of<512>();
+    case 1024: return threads_of<1024>();
+    }
+    return 0;
+}
+
 int pipe_block_of(int W)
 {
     switch (W) {
@@ -1932,7 +1962,7 @@ int pipe_max_resident_blocks(int W, bool sweep)
     if (!fn) return -1;
     const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, W > 16 ? 6 * kWave : 5 * kWave, dyn) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, pipe_threads(W), dyn) !=
         hipSuccess)
         return -3;
     if (W == 16) {  // the paired-halves build of the same plan must fit as well
@@ -1959,7 +1989,7 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;
     PipeArgs args = a;
     void *kargs[] = {&args};
-    const int threads = W > 16 ? 6 * kWave : 5 * kWave;
+    const int threads = pipe_threads(W);
     if (hipLaunchKernel(fn, dim3(blocks), dim3(threads), kargs, dyn, st) != hipSuccess) return -3;
     return hipGetLastError() == hipSuccess ? 0 : -3;
 }

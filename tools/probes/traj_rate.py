@@ -1,6 +1,7 @@
 """Rate of burg_trajectory_ex on one GPU: python traj_rate.py NX NY [snap_every] [reps]
 (dt = 0.05 * 1024 / NX as the bench; one warm-up, then reps timed launches;
-prints one JSON line; the A/B knobs are environment variables)."""
+prints one JSON line; the A/B knobs are environment variables; TRAJ_W forces
+the tile width)."""
 import json
 import os
 import sys
@@ -15,7 +16,7 @@ nx, ny = int(sys.argv[1]), int(sys.argv[2])
 k = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 reps = int(sys.argv[4]) if len(sys.argv) > 4 else 3
 T = 500
-ctx = FOMContext(nx, ny)
+ctx = FOMContext(nx, ny, stream_w=int(os.environ.get("TRAJ_W", "0")))
 ctx.set_problem(np.linspace(0, 100, nx + 1), np.linspace(0, 100.0 * ny / nx, ny + 1),
                 0.05 * 1024 / nx, (5.19, 0.026), allow_nonsquare=nx != ny)
 ctx.upload(np.ones(ctx.m))
