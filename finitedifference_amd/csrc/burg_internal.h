@@ -183,6 +183,9 @@ struct StreamArgs {
 #define BURG_PIPE_R 8
 #endif
 constexpr int kPipeR = BURG_PIPE_R;  // global mailbox slots (steps) per edge, power of two
+// (8 is the only depth run and tested; a 16-step build failed its first wait
+// in round 5, profiles/r05/ab/narrow/r16_error.txt -- refuse other depths)
+static_assert(kPipeR == 8, "BURG_PIPE_R: only 8-step mailboxes are supported");
 constexpr int kPipeRL = 4;  // LDS ring slots (steps) per intra-workgroup edge
 constexpr int kPipeSweepMax = 9;   // trajectories per sweep launch (LDS-resident tables)
 
