@@ -7,6 +7,7 @@
 //                   of the reference's snaps matrix (:89-90, :126)
 // Op order of residual/jvp mirrors oracle/burgers_oracle.c (compiled with
 // -ffp-contract=off on both sides), so GPU == oracle bit for bit.
+#include <algorithm>
 #include <cstdlib>
 
 #include "burg_internal.h"
@@ -322,7 +323,9 @@ __global__ __launch_bounds__(256) void transpose_kernel(StatePtrs sp, int nstate
 }  // namespace
 
 // Stencil variant (A/B knob BURG_STENCIL, bits: 1 XCD-aware block order, 2
-// next-row prefetch).  Every variant computes the same cells with the same op
+// next-row prefetch, 4 resident layout: as many row blocks as the chip holds
+// at once, so every block is in flight from the start and there is no tail;
+// rows per block follow, e.g. 128 at 8192^2).  Every variant computes the same cells with the same op
 // order: the results are bit-identical.  Measured at 8192^2 (round 4,
 // profiles/r04/stencil_ab_v1): residual 0.635 / 0.636 / 0.640 / 0.640 ms,
 // J.x 0.624 / 0.625 / 0.622 / 0.626 ms for variants 0 / 1 / 2 / 3 -- neither
@@ -336,7 +339,7 @@ int stencil_variant()
     static int v = -1;
     if (v < 0) {
         v = BURG_STENCIL_DEFAULT;
-        if (const char *e = std::getenv("BURG_STENCIL")) v = std::atoi(e) & 3;
+        if (const char *e = std::getenv("BURG_STENCIL")) v = std::atoi(e) & 7;
     }
     return v;
 }
@@ -353,7 +356,17 @@ int stencil_variant()
 struct StencilLayout {
     int nbx, rows, nb;
 };
-static StencilLayout stencil_layout(const Coeffs &cf)
+// workgroups of `fn` resident on the whole GPU at once (0: unknown)
+static int resident_blocks(const void *fn)
+{
+    int dev = 0, ncu = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, 0) != hipSuccess)
+        return 0;
+    return n * ncu;
+}
+static StencilLayout stencil_layout(const Coeffs &cf, const void *fn)
 {
     static int force = -1;
     if (force < 0) {
@@ -364,23 +377,52 @@ static StencilLayout stencil_layout(const Coeffs &cf)
     l.nbx = (cf.nx + kBlock - 1) / kBlock;
     l.rows = 64;
     while (l.rows > 8 && (long long)l.nbx * ((cf.ny + l.rows - 1) / l.rows) < 16384) l.rows >>= 1;
+    if (stencil_variant() & 4) {
+        static const void *fn_c = nullptr;
+        static int cap_c = 0;
+        if (fn != fn_c) fn_c = fn, cap_c = resident_blocks(fn);
+        if (cap_c > 0) {
+            const int nby = std::max(1, cap_c / l.nbx);
+            l.rows = (cf.ny + nby - 1) / nby;
+        }
+    }
     if (force >= 1 && force <= 1024) l.rows = force;
     l.nb = l.nbx * ((cf.ny + l.rows - 1) / l.rows);
     return l;
 }
 
-int residual_partials_count(const Coeffs &cf) { return stencil_layout(cf).nb; }
+// the residual kernel of the current variant (its layout sizes the partials)
+static const void *residual_fn()
+{
+    switch (stencil_variant() & 3) {
+    case 0: return (const void *)residual_kernel<false, false>;
+    case 1: return (const void *)residual_kernel<true, false>;
+    case 2: return (const void *)residual_kernel<false, true>;
+    default: return (const void *)residual_kernel<true, true>;
+    }
+}
+static const void *jvp_fn()
+{
+    switch (stencil_variant() & 3) {
+    case 0: return (const void *)jvp_kernel<false, false>;
+    case 1: return (const void *)jvp_kernel<true, false>;
+    case 2: return (const void *)jvp_kernel<false, true>;
+    default: return (const void *)jvp_kernel<true, true>;
+    }
+}
+
+int residual_partials_count(const Coeffs &cf) { return stencil_layout(cf, residual_fn()).nb; }
 
 int launch_residual(const Coeffs &cf, const double *w, const double *wp, double *r,
                     double *partials, double *sumsq, const double *halo_w,
                     const double *halo_wp, hipStream_t st)
 {
-    const StencilLayout l = stencil_layout(cf);
+    const StencilLayout l = stencil_layout(cf, residual_fn());
     const int rows = l.rows, nbx = l.nbx, nb = l.nb;
     // (round 4: the final sum fused into the last block -- an agent-scope
     // ticket, sc1 partials -- measured the same as this second launch,
     // profiles/r04/stencil_ab_v4, and was not kept)
-    switch (stencil_variant()) {
+    switch (stencil_variant() & 3) {
     case 0: residual_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
     case 1: residual_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
     case 2: residual_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, wp, r, partials, halo_w, halo_wp, rows, nbx, nb); break;
@@ -392,9 +434,9 @@ int launch_residual(const Coeffs &cf, const double *w, const double *wp, double 
 
 int launch_jvp(const Coeffs &cf, const double *w, const double *x, double *y, hipStream_t st)
 {
-    const StencilLayout l = stencil_layout(cf);
+    const StencilLayout l = stencil_layout(cf, jvp_fn());
     const int rows = l.rows, nbx = l.nbx, nb = l.nb;
-    switch (stencil_variant()) {
+    switch (stencil_variant() & 3) {
     case 0: jvp_kernel<false, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
     case 1: jvp_kernel<true, false><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
     case 2: jvp_kernel<false, true><<<nb, kBlock, 0, st>>>(cf, w, x, y, rows, nbx, nb); break;
