@@ -378,11 +378,9 @@ static StencilLayout stencil_layout(const Coeffs &cf, const void *fn)
     l.rows = 64;
     while (l.rows > 8 && (long long)l.nbx * ((cf.ny + l.rows - 1) / l.rows) < 16384) l.rows >>= 1;
     if (stencil_variant() & 4) {
-        static const void *fn_c = nullptr;
-        static int cap_c = 0;
-        if (fn != fn_c) fn_c = fn, cap_c = resident_blocks(fn);
-        if (cap_c > 0) {
-            const int nby = std::max(1, cap_c / l.nbx);
+        const int cap = resident_blocks(fn);  // (per call: the current device's)
+        if (cap > 0) {
+            const int nby = std::max(1, cap / l.nbx);
             l.rows = (cf.ny + nby - 1) / nby;
         }
     }
