@@ -94,6 +94,12 @@ constexpr unsigned kLdsEmptyHi = 0x7FF6DEADu;  // LDS slot empty
 constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, stores dropped
 constexpr int kR = kPipeR;
 constexpr unsigned G = kPipeGranuleStride;
+// BURG_DMA_READBACK: the loader reads each block's LDS-DMA bytes back before
+// it publishes filled[] (see the loader wave).  0 = rounds 2-4's protocol,
+// which races (A/B and race probe only).
+#ifndef BURG_DMA_READBACK
+#define BURG_DMA_READBACK 1
+#endif
 // BURG_LOADERS: loader waves per wide workgroup.  2 (round 5) = wave 5 fills
 // compute waves 0-1's windows, wave 6 those of waves 2-3: twice the ring DMAs
 // in flight per workgroup (one wave keeps at most 63 loads outstanding, and
@@ -272,11 +278,21 @@ __device__ __forceinline__ bool l_is_data(v4u g) { return g.y != kLdsEmptyHi && 
 // lane i <- lane i-1; lane 0 keeps `old0`
 __device__ __forceinline__ double shr1_or(double old0, double x)
 {
+#ifdef BURG_SHR_BPERMUTE
+    // (race diagnosis: the LDS crossbar instead of DPP wave_shr)
+    const int l = (int)__lane_id();
+    const int addr = ((l + 63) & 63) * 4;
+    const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(x));
+    const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(x));
+    const double y = __hiloint2double(hi, lo);
+    return l == 0 ? old0 : y;
+#else
     const int lo = __builtin_amdgcn_update_dpp(__double2loint(old0), __double2loint(x), 0x138,
                                                0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old0), __double2hiint(x), 0x138,
                                                0xf, 0xf, false);
     return __hiloint2double(hi, lo);
+#endif
 }
 
 // device mailboxes: sc1 (agent scope, write-through, L1 bypass);
@@ -350,6 +366,10 @@ __device__ __forceinline__ void lds_st(LDS v4u *p, v4u v) { *(volatile lds_v4u *
 __device__ __forceinline__ unsigned lds_ld32(const LDS void *p) { return *(volatile const lds_u32 *)p; }
 __device__ __forceinline__ int lds_ldi(const LDS int *p) { return *(volatile const lds_i32 *)p; }
 __device__ __forceinline__ void lds_sti(LDS int *p, int v) { *(volatile lds_i32 *)p = v; }
+// Opaque copy of a store's offset and data: the store then reads exactly the
+// VGPRs the caller keeps live afterwards (no immediate-offset folding, no
+// in-place offset increments) -- see keep_stores in the compute waves.
+__device__ __forceinline__ void launder(unsigned &off, v4u &v) { asm volatile("" : "+v"(off), "+v"(v)); }
 
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
@@ -449,7 +469,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     constexpr int kRL = rl_of<W>();
     constexpr int kLA = la_of<W>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
+#ifdef BURG_WAVE_SWAP14
+    // (race diagnosis: compute wave 1 and the comm wave trade hardware slots)
+    const int hw_wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = hw_wave == 1 ? 4 : hw_wave == 4 ? 1 : hw_wave;
+#else
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#endif
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
     // a.wg_cm (host: pipe_args): column-major, workgroup i -> tile row i % nti,
@@ -566,7 +592,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
 
     if (wave == 4) {
         // ================= comm wave =================
-        __builtin_amdgcn_s_setprio(0);
+#ifndef BURG_COMM_PRIO
+#define BURG_COMM_PRIO 0
+#endif
+        __builtin_amdgcn_s_setprio(BURG_COMM_PRIO);
         // south / north streams: lane = kS * 16 + jS handles the diagonals
         // jS (mod 16) of wave kS's tile
         const int kS = lane >> 4, jS = lane & (kSL - 1);
@@ -591,9 +620,17 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const unsigned sWEstep = (unsigned)kWave * G;
         const int kq = kS & 3;
         int qs = jS, qn = jS, qw = 0, qe = 0;  // qs, qn: diagonals; qw, qe: steps
+#ifdef BURG_COMM_WRITE_CHANGED
+        int lastN = -1, lastE = -1;
+#endif
         long long t_prog = now_rt();
         unsigned long long iters = 0;
+        // the previous iteration's sentinel stores (data, offsets), kept live
+        // until this one's (see keep_stores in the compute waves)
+        v4u kc_s = v4u{0u, 0u, 0u, 0u}, kc_w = kc_s;
+        unsigned kc_os = 0u, kc_ow = 0u;
         for (;;) {
+            asm volatile("" ::"v"(kc_s), "v"(kc_w), "v"(kc_os), "v"(kc_ow));
             const bool rS = actS && qs < KW, rN = actN && qn < KW;
             const bool rW = actW && qw < K, rE = actE && qe < K;
             if (!__any(rS || rN || rW || rE)) break;
@@ -634,9 +671,13 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 LDS v4u *slot = &sm.ins[kq][qs & (kNI - 1)];
                 if (!l_is_data(lds_ld(slot))) {
                     lds_st(slot, gS);
-                    const v4u e = sent_g(((aS / kR) & 1) ^ 1);
-                    if (south_host) st_sys(hin, oS, e);  // (virtual: oS is OOB, dropped)
-                    else st_dev(sbox, oS, e);
+                    v4u e = sent_g(((aS / kR) & 1) ^ 1);
+                    unsigned os = oS;
+                    launder(os, e);
+                    if (south_host) st_sys(hin, os, e);  // (virtual: oS is OOB, dropped)
+                    else st_dev(sbox, os, e);
+                    kc_s = e;
+                    kc_os = os;
                     qs += kSL;
                     prog = true;
                 }
@@ -645,7 +686,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 LDS v4u *slot = &sm.inw[qw & (kRL - 1)][lane];
                 if (!l_is_data(lds_ld(slot))) {
                     lds_st(slot, gW);
-                    st_dev(wbox, oW, sent_g(((aW / kR) & 1) ^ 1));
+                    kc_w = sent_g(((aW / kR) & 1) ^ 1);
+                    kc_ow = oW;
+                    launder(kc_ow, kc_w);
+                    st_dev(wbox, kc_ow, kc_w);
                     ++qw;
                     prog = true;
                 }
@@ -663,8 +707,16 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // minimum over rows would tie row 0's progress to row 63's)
             int vN = actN ? qn : INT_MAX;
             for (int m = 1; m < kSL; m <<= 1) vN = min(vN, __shfl_xor(vN, m));
+#ifdef BURG_COMM_WRITE_CHANGED
+            // (only what changed: no LDS store per poll)
+            if (jS == 0 && kval && vN != lastN) lds_sti(&sm.perm[kq], vN);
+            if (actE && qe != lastE) lds_sti(&sm.pe_row[lane], qe);
+            lastN = vN;
+            lastE = qe;
+#else
             if (jS == 0 && kval) lds_sti(&sm.perm[kq], vN);
             if (actE) lds_sti(&sm.pe_row[lane], qe);
+#endif
             const long long tn = now_rt();
             if (__any(prog) || !__any(wS || wN || wW || wE)) {
                 t_prog = tn;  // progress, or nothing due (the compute waves time out themselves)
@@ -744,15 +796,26 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                         const int sl = nf[k] & (kCCW - 1);
                         const unsigned co = (unsigned)((nf[k] + lane) & (W - 1)) * 16u;
                         if (lane < U) {
+#ifdef BURG_LOADER_VGPR
+                            const v4u cx = ld_dev(colc, co);
+                            lds_st(&sm.cc[k][sl + lane], cx);
+                            lds_st(&sm.cc[k][(sl == 0 ? kCCW : sl) + lane], cx);
+#else
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl], 16, co, 0, 0, 0);
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl == 0 ? kCCW : sl], 16,
                                                                      co, 0, 0, 0);
+#endif
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
+#ifdef BURG_LOADER_VGPR
+                        // (race diagnosis: the ring rows through VGPRs + ds_write)
+                        lds_st(&sm.win[k][slot][lane], ld_dev(ring, (unsigned)e * 1024u + lane * 16u));
+#else
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
                                                                  (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
+#endif
                         e = e + 1 == L ? 0 : e + 1;
                         slot = slot + 1 == KWIN ? 0 : slot + 1;
                     }
@@ -776,6 +839,27 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     case 1: wait_vmcnt<NB>(); break;
                     case 2: wait_vmcnt<2 * NB>(); break;
                     default: wait_vmcnt<3 * NB>(); break;
+                    }
+                    // Read the block's DMA'd bytes back before publishing them:
+                    // an LDS-DMA write is ordered only for the ISSUING wave's
+                    // own LDS reads behind its covering vmcnt (MI355X_MICROARCH.md
+                    // item 7); the reads return only after the writes they are
+                    // ordered behind, and the flag store waits for the reads.
+                    // (Defensive: round 5's wrong window rows turned out to be
+                    // the ring stores' VGPR hazard)
+                    if constexpr (BURG_DMA_READBACK) {
+                        v4u acc = v4u{0u, 0u, 0u, 0u};
+                        const int s0 = (nf[k] - U) % KWIN;
+#pragma unroll
+                        for (int j = 0; j < U; ++j) acc ^= lds_ld(&sm.win[k][s0 + j][lane]);
+                        if constexpr (ccw_of<W>()) {
+                            const int sl = (nf[k] - U) & (kCCW - 1);
+                            if (lane < U) {
+                                acc ^= lds_ld(&sm.cc[k][sl + lane]);
+                                acc ^= lds_ld(&sm.cc[k][(sl == 0 ? kCCW : sl) + lane]);
+                            }
+                        }
+                        asm volatile("" ::"v"(acc));  // (the s_waitcnt lgkmcnt for the reads lands here)
                     }
                     if (lane == 0) lds_sti(&sm.filled[k], nf[k]);
                 }
@@ -889,6 +973,14 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         unsigned long long pspins = 0, pslow = 0, pieee = 0, pnonfin = 0, pwait = 0;
         unsigned pwhy[5] = {0, 0, 0, 0, 0};
         bool paborted = false;
+        // the previous paired diagonal's store data and offsets, kept live
+        // until this one's stores (see keep_stores in the one-cell kernel)
+        v4u kq_a = v4u{0u, 0u, 0u, 0u}, kq_b = kq_a, kq_e = kq_a, kq_na = kq_a, kq_nb = kq_a;
+        unsigned kq_ra = 0u, kq_rb = 0u, kq_eo = 0u, kq_oa = 0u, kq_ob = 0u;
+        auto keep_prev = [&]() {
+            asm volatile("" ::"v"(kq_a), "v"(kq_b), "v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_ra), "v"(kq_rb),
+                         "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
+        };
         // missing inflows / grants of block [sb, sb + 8): name_it = false: any
         // (one ballot); true: the kinds (bits as err[3] >> 8)
         auto missing2 = [&](int sb, bool name_it) -> unsigned {
@@ -1014,27 +1106,50 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             if (tau >= 0) my_st[sl * kWave + lane] = outA;
             if (tau >= 8) my_st[(8 + sl) * kWave + lane] = outB;
             const unsigned eB = eA >= 8u ? eA - 8u : eA + Lu - 8u;
-            st_plain(ring, vA ? eA * 1024u + lane16 : kOOB, outA);
-            st_plain(ring, vB ? eB * 1024u + lane16 : kOOB, outB);
+            keep_prev();
+            unsigned ra = vA ? eA * 1024u + lane16 : kOOB, rb = vB ? eB * 1024u + lane16 : kOOB;
+            v4u ka = outA, kb = outB;
+            launder(ra, ka);
+            launder(rb, kb);
+            st_plain(ring, ra, ka);
+            st_plain(ring, rb, kb);
             eA += atE ? 9u : 1u;
             if (eA >= Lu) eA -= Lu;
             // east edge: B's column 15 (step qB)
             const bool out_e = atE & vB & rowok;
-            const v4u eo = as_v4u(oeB0, oeB1);
+            v4u eo = as_v4u(oeB0, oeB1);
             if (east_lds) lds_st(out_e ? &sm.ewe[k][qB & (kRL - 1)][lane] : dumpv, eo);
-            if (east_glob) st_dev(wbox, out_e ? eb + (unsigned)((a.qbase + qB) & (kR - 1)) * (kWave * G) : kOOB, eo);
+            unsigned eoff = kOOB;
+            if (east_glob) {
+                eoff = out_e ? eb + (unsigned)((a.qbase + qB) & (kR - 1)) * (kWave * G) : kOOB;
+                launder(eoff, eo);
+                st_dev(wbox, eoff, eo);
+            }
+            unsigned offA = kOOB, offB = kOOB;
             // north edge: the top lane's A (step qA, column cA) and B (qB, 8 + cA)
             if (has_north) {
                 const bool tl = lane == top;
-                const unsigned offA = (tl & vA & (cA < ncol_real))
-                                          ? nb + (unsigned)((a.qbase + qA) & (kR - 1)) * nstep + (unsigned)cA * ncol
-                                          : kOOB;
-                const unsigned offB = (tl & vB & (8 + cA < ncol_real))
-                                          ? nb + (unsigned)((a.qbase + qB) & (kR - 1)) * nstep + (unsigned)(8 + cA) * ncol
-                                          : kOOB;
-                st_sys(nrs, offA, as_v4u(onA0, onA1));
-                st_sys(nrs, offB, as_v4u(onB0, onB1));
+                offA = (tl & vA & (cA < ncol_real))
+                           ? nb + (unsigned)((a.qbase + qA) & (kR - 1)) * nstep + (unsigned)cA * ncol
+                           : kOOB;
+                offB = (tl & vB & (8 + cA < ncol_real))
+                           ? nb + (unsigned)((a.qbase + qB) & (kR - 1)) * nstep + (unsigned)(8 + cA) * ncol
+                           : kOOB;
+                kq_na = as_v4u(onA0, onA1);
+                kq_nb = as_v4u(onB0, onB1);
+                launder(offA, kq_na);
+                launder(offB, kq_nb);
+                st_sys(nrs, offA, kq_na);
+                st_sys(nrs, offB, kq_nb);
             }
+            kq_a = ka;
+            kq_b = kb;
+            kq_e = eo;
+            kq_ra = ra;
+            kq_rb = rb;
+            kq_eo = eoff;
+            kq_oa = offA;
+            kq_ob = offB;
             // the consumed west granule back to empty
             if (has_west) {
                 const bool need_w = at0 & vA & rowok;
@@ -1140,14 +1255,37 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                 const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
                 my_st[u * kWave + lane] = outA;
                 my_st[(8 + u) * kWave + lane] = outB;
-                const unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u;
-                st_plain(ring, rA, outA);
-                st_plain(ring, rA - 8192u, outB);
-                const v4u eo = as_v4u(oeB0, oeB1);
+                keep_prev();
+                unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u, rB = rA - 8192u;
+                v4u ka = outA, kb = outB;
+                launder(rA, ka);
+                launder(rB, kb);
+                st_plain(ring, rA, ka);
+                st_plain(ring, rB, kb);
+                v4u eo = as_v4u(oeB0, oeB1);
                 lds_st(atE ? eaddr : dumpv, eo);
-                if (east_glob) st_dev(wbox, atE ? eoff : kOOB, eo);
-                st_sys(nrs, (u < uw8 ? nA1 : nA2) + (unsigned)u * ncol, as_v4u(onA0, onA1));
-                st_sys(nrs, (u < uw8 ? nB1 : nB2) + (unsigned)u * ncol, as_v4u(onB0, onB1));
+                unsigned eo_off = atE ? eoff : kOOB;
+                if (east_glob) {
+                    launder(eo_off, eo);
+                    st_dev(wbox, eo_off, eo);
+                }
+                unsigned oa = (u < uw8 ? nA1 : nA2) + (unsigned)u * ncol;
+                unsigned ob = (u < uw8 ? nB1 : nB2) + (unsigned)u * ncol;
+                v4u na = as_v4u(onA0, onA1), nbv = as_v4u(onB0, onB1);
+                launder(oa, na);
+                launder(ob, nbv);
+                st_sys(nrs, oa, na);
+                st_sys(nrs, ob, nbv);
+                kq_a = ka;
+                kq_b = kb;
+                kq_e = eo;
+                kq_na = na;
+                kq_nb = nbv;
+                kq_ra = rA;
+                kq_rb = rB;
+                kq_eo = eo_off;
+                kq_oa = oa;
+                kq_ob = ob;
             }
             if (has_west) lds_st(&src_w[qw & (kRL - 1)][lane], lempty);
             eA += 16u;
@@ -1234,6 +1372,10 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     }
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
+    // the previous diagonal's store data and offsets, kept live until this
+    // diagonal's stores (keep_stores below)
+    v4u kp_out = v4u{0u, 0u, 0u, 0u}, kp_e = kp_out, kp_n = kp_out;
+    unsigned kp_ro = 0u, kp_eo = 0u, kp_no = 0u;
     unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0, wait_ticks = 0;
     unsigned wait_why[5] = {0, 0, 0, 0, 0};  // blocks that waited, by first missing kind
     bool aborted = false;
@@ -1515,19 +1657,33 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         if constexpr (!WIDE) {
             if (STEADY || t >= 0) my_st[(s & (W - 1)) * kWave + lane] = out;
         }
+        // Store VGPRs are not reused before the NEXT diagonal's stores: a
+        // buffer store reads its data / offset VGPRs after it issues, and
+        // under load on the CU's memory pipeline that read has come after a
+        // following VALU overwrote them (round 5: ring entries with u = 0.5
+        // -- the next cell's 0.5 * pu -- in lanes 12-15 of every 16, once the
+        // comm wave ran at a higher priority)
+        asm volatile("" ::"v"(kp_out), "v"(kp_e), "v"(kp_n), "v"(kp_ro), "v"(kp_eo), "v"(kp_no));
         // wide tiles: the loader wave reads this entry back (sc1 DMA) W
         // diagonals later, so it is stored write-through to L2 (sc1): the
         // store's vmcnt then completes at L2, which the done[] protocol needs
+        unsigned ro;        // the ring store's voffset
+        unsigned eoff = kOOB, noff = kOOB;  // the east / north stores' voffsets
+        v4u outk = out;
         if constexpr (STEADY) {
-            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(out, ring, lane16, pw * 1024u, BURG_RING_AUX);
-            else st_plain_so(ring, lane16, pw * 1024u, out);
+            ro = lane16;
+            launder(ro, outk);
+            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(outk, ring, ro, pw * 1024u, BURG_RING_AUX);
+            else st_plain_so(ring, ro, pw * 1024u, outk);
             ++pw;  // (no wrap inside a steady block)
         } else {
-            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(out, ring, valid ? pw * 1024u + lane16 : kOOB, 0, BURG_RING_AUX);
-            else st_plain(ring, valid ? pw * 1024u + lane16 : kOOB, out);
+            ro = valid ? pw * 1024u + lane16 : kOOB;
+            launder(ro, outk);
+            if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(outk, ring, ro, 0, BURG_RING_AUX);
+            else st_plain(ring, ro, outk);
             pw = pw + 1 == Lu ? 0u : pw + 1;
         }
-        const v4u eo = as_v4u(oe0, oe1);
+        v4u eo = as_v4u(oe0, oe1);
         const int aq = a.qbase + q;
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
@@ -1546,32 +1702,49 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // narrow: unconditional too -- se_eoff is out of range unless this is
             // the workgroup's east wave -- a dropped store costs less than the
             // two taken branches around a conditional one)
-            if (WIDE || SE_G) st_dev(wbox, atE ? se_eoff : kOOB, eo);
+            if (WIDE || SE_G) {
+                eoff = atE ? se_eoff : kOOB;
+                launder(eoff, eo);
+                st_dev(wbox, eoff, eo);
+            }
         }
-        else if (EDGE && (WIDE || east_glob))
-            st_dev(wbox, east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB, eo);
+        else if (EDGE && (WIDE || east_glob)) {
+            eoff = east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB;
+            launder(eoff, eo);
+            st_dev(wbox, eoff, eo);
+        }
         // (narrow steady blocks store unconditionally: nv1 / nv2 are out of
         // range on every lane but a north-writing top lane)
         if (WIDE || STEADY || has_north) {
             // one store flavour for both targets: sc0 sc1 (system scope) reaches
             // the host / peer halo ring and is write-through like sc1 for the
             // device mailboxes (consumers poll with sc1 / sc0 sc1 loads)
-            const v4u no = as_v4u(on0, on1);
+            v4u no = as_v4u(on0, on1);
             if constexpr (STEADY) {
                 // the top lane's slot: SGPR offset, advanced one column per diagonal
                 if constexpr (WIDE) {
-                    st_sys_so(nrs, (has_north & (lane == top)) ? 0u : kOOB, noffs, no);
+                    noff = (has_north & (lane == top)) ? 0u : kOOB;
+                    launder(noff, no);
+                    st_sys_so(nrs, noff, noffs, no);
                     noffs += ncol;
                 } else {
-                    st_sys(nrs, (u < uwrap ? nv1 : nv2) + (unsigned)u * ncol, no);
+                    noff = (u < uwrap ? nv1 : nv2) + (unsigned)u * ncol;
+                    launder(noff, no);
+                    st_sys(nrs, noff, no);
                 }
             } else {
-                const unsigned off = (out_n & (c < ncol_real))
-                                         ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
-                                         : kOOB;
-                st_sys(nrs, off, no);
+                noff = (out_n & (c < ncol_real)) ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
+                                                 : kOOB;
+                launder(noff, no);
+                st_sys(nrs, noff, no);
             }
+            kp_n = no;
         }
+        kp_out = outk;
+        kp_e = eo;
+        kp_ro = ro;
+        kp_eo = eoff;
+        kp_no = noff;
         // consumed inbound slots back to empty (steady-edge blocks: once per
         // block, run_block)
         if constexpr (WIDE || STEADY) {
@@ -1683,7 +1856,11 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // (2 or 3 stores per diagonal, no loads: waiting down to the smaller
             // count, 2 U, covers both kinds of predecessor): the loader may read
             // ring entries written before diagonal sb - U
+#ifdef BURG_DONE_DRAIN
+            wait_vmcnt<0>();  // (race diagnosis: every store drained before done[])
+#else
             wait_vmcnt<2 * U>();
+#endif
 #ifdef BURG_PIPE_PROF
             pf_vm += __builtin_amdgcn_s_memtime() - pfa;
 #endif

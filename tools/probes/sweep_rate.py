@@ -25,5 +25,11 @@ sw = [r["loop_ms"] for r in res]
 print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("BURG_")},
                   "sweep9_ms": [round(x, 3) for x in sw],
                   "sweep9_gcell": round(9 * N * N * T / min(sw) / 1e6, 1),
-                  "launches": res[-1].get("stream_launches"), "paired": res[-1].get("paired_launches")}),
+                  "launches": res[-1].get("stream_launches"), "paired": res[-1].get("paired_launches"),
+                  # compute-wave time spent waiting at block readiness (s_memtime:
+                  # shader clock cycles, taken at the measured 2.176 GHz) over
+                  # compute-wave time (one wave per tile)
+                  "slow_blocks": res[-1].get("slow_diagonals"), "slow_ticks": res[-1].get("slow_ticks"),
+                  "wait_frac": (round(res[-1]["slow_ticks"] / 2.176e9 / (sw[-1] * 1e-3 * res[-1]["stream_tiles"]), 4)
+                                if res[-1].get("slow_ticks") else None)}),
       flush=True)
