@@ -278,21 +278,11 @@ __device__ __forceinline__ bool l_is_data(v4u g) { return g.y != kLdsEmptyHi && 
 // lane i <- lane i-1; lane 0 keeps `old0`
 __device__ __forceinline__ double shr1_or(double old0, double x)
 {
-#ifdef BURG_SHR_BPERMUTE
-    // (race diagnosis: the LDS crossbar instead of DPP wave_shr)
-    const int l = (int)__lane_id();
-    const int addr = ((l + 63) & 63) * 4;
-    const int lo = __builtin_amdgcn_ds_bpermute(addr, __double2loint(x));
-    const int hi = __builtin_amdgcn_ds_bpermute(addr, __double2hiint(x));
-    const double y = __hiloint2double(hi, lo);
-    return l == 0 ? old0 : y;
-#else
     const int lo = __builtin_amdgcn_update_dpp(__double2loint(old0), __double2loint(x), 0x138,
                                                0xf, 0xf, false);
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old0), __double2hiint(x), 0x138,
                                                0xf, 0xf, false);
     return __hiloint2double(hi, lo);
-#endif
 }
 
 // device mailboxes: sc1 (agent scope, write-through, L1 bypass);
@@ -469,13 +459,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
     constexpr int kRL = rl_of<W>();
     constexpr int kLA = la_of<W>();
     LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
-#ifdef BURG_WAVE_SWAP14
-    // (race diagnosis: compute wave 1 and the comm wave trade hardware slots)
-    const int hw_wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wave = hw_wave == 1 ? 4 : hw_wave == 4 ? 1 : hw_wave;
-#else
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#endif
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
     // a.wg_cm (host: pipe_args): column-major, workgroup i -> tile row i % nti,
@@ -620,9 +604,6 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
         const unsigned sWEstep = (unsigned)kWave * G;
         const int kq = kS & 3;
         int qs = jS, qn = jS, qw = 0, qe = 0;  // qs, qn: diagonals; qw, qe: steps
-#ifdef BURG_COMM_WRITE_CHANGED
-        int lastN = -1, lastE = -1;
-#endif
         long long t_prog = now_rt();
         unsigned long long iters = 0;
         // the previous iteration's sentinel stores (data, offsets), kept live
@@ -707,16 +688,8 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // minimum over rows would tie row 0's progress to row 63's)
             int vN = actN ? qn : INT_MAX;
             for (int m = 1; m < kSL; m <<= 1) vN = min(vN, __shfl_xor(vN, m));
-#ifdef BURG_COMM_WRITE_CHANGED
-            // (only what changed: no LDS store per poll)
-            if (jS == 0 && kval && vN != lastN) lds_sti(&sm.perm[kq], vN);
-            if (actE && qe != lastE) lds_sti(&sm.pe_row[lane], qe);
-            lastN = vN;
-            lastE = qe;
-#else
             if (jS == 0 && kval) lds_sti(&sm.perm[kq], vN);
             if (actE) lds_sti(&sm.pe_row[lane], qe);
-#endif
             const long long tn = now_rt();
             if (__any(prog) || !__any(wS || wN || wW || wE)) {
                 t_prog = tn;  // progress, or nothing due (the compute waves time out themselves)
@@ -796,26 +769,15 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                         const int sl = nf[k] & (kCCW - 1);
                         const unsigned co = (unsigned)((nf[k] + lane) & (W - 1)) * 16u;
                         if (lane < U) {
-#ifdef BURG_LOADER_VGPR
-                            const v4u cx = ld_dev(colc, co);
-                            lds_st(&sm.cc[k][sl + lane], cx);
-                            lds_st(&sm.cc[k][(sl == 0 ? kCCW : sl) + lane], cx);
-#else
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl], 16, co, 0, 0, 0);
                             __builtin_amdgcn_raw_ptr_buffer_load_lds(colc, (LDS void *)&sm.cc[k][sl == 0 ? kCCW : sl], 16,
                                                                      co, 0, 0, 0);
-#endif
                         }
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-#ifdef BURG_LOADER_VGPR
-                        // (race diagnosis: the ring rows through VGPRs + ds_write)
-                        lds_st(&sm.win[k][slot][lane], ld_dev(ring, (unsigned)e * 1024u + lane * 16u));
-#else
                         __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
                                                                  (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
-#endif
                         e = e + 1 == L ? 0 : e + 1;
                         slot = slot + 1 == KWIN ? 0 : slot + 1;
                     }
@@ -1856,11 +1818,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
             // (2 or 3 stores per diagonal, no loads: waiting down to the smaller
             // count, 2 U, covers both kinds of predecessor): the loader may read
             // ring entries written before diagonal sb - U
-#ifdef BURG_DONE_DRAIN
-            wait_vmcnt<0>();  // (race diagnosis: every store drained before done[])
-#else
             wait_vmcnt<2 * U>();
-#endif
 #ifdef BURG_PIPE_PROF
             pf_vm += __builtin_amdgcn_s_memtime() - pfa;
 #endif
