@@ -356,10 +356,14 @@ __device__ __forceinline__ void lds_st(LDS v4u *p, v4u v) { *(volatile lds_v4u *
 __device__ __forceinline__ unsigned lds_ld32(const LDS void *p) { return *(volatile const lds_u32 *)p; }
 __device__ __forceinline__ int lds_ldi(const LDS int *p) { return *(volatile const lds_i32 *)p; }
 __device__ __forceinline__ void lds_sti(LDS int *p, int v) { *(volatile lds_i32 *)p = v; }
-// Opaque copy of a store's offset and data: the store then reads exactly the
-// VGPRs the caller keeps live afterwards (no immediate-offset folding, no
-// in-place offset increments) -- see keep_stores in the compute waves.
-__device__ __forceinline__ void launder(unsigned &off, v4u &v) { asm volatile("" : "+v"(off), "+v"(v)); }
+// Opaque copy of a store's offset: the store then reads exactly the VGPR the
+// caller keeps live afterwards (no immediate-offset folding, no in-place
+// offset increments); the data VGPRs are the kept values themselves -- see
+// the store VGPR note in the compute waves.
+__device__ __forceinline__ void launder(unsigned &off, v4u &) { asm volatile("" : "+v"(off)); }
+// (the comm wave: its data too -- a phi over two store branches let the
+// compiler keep a copy and reuse the stored registers)
+__device__ __forceinline__ void launder_all(unsigned &off, v4u &v) { asm volatile("" : "+v"(off), "+v"(v)); }
 
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
@@ -654,7 +658,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     lds_st(slot, gS);
                     v4u e = sent_g(((aS / kR) & 1) ^ 1);
                     unsigned os = oS;
-                    launder(os, e);
+                    launder_all(os, e);
                     if (south_host) st_sys(hin, os, e);  // (virtual: oS is OOB, dropped)
                     else st_dev(sbox, os, e);
                     kc_s = e;
@@ -669,7 +673,7 @@ __global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
                     lds_st(slot, gW);
                     kc_w = sent_g(((aW / kR) & 1) ^ 1);
                     kc_ow = oW;
-                    launder(kc_ow, kc_w);
+                    launder_all(kc_ow, kc_w);
                     st_dev(wbox, kc_ow, kc_w);
                     ++qw;
                     prog = true;
