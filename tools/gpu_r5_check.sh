@@ -15,4 +15,8 @@ echo smoke ok
 timeout -k 10 400 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
 echo bench ok
 timeout -k 10 300 python bench.py --nx 16384 --rows-per-gpu 2048 --snap-every 10 --steps 3 --warmup 1 --no-1024 --no-rom --no-cpu-baseline --stencil-nx 0 --no-e2e > $O/slab_16384x2048.json 2> $O/slab.err || { tail -20 $O/slab.err; exit 1; }
-echo ALLOK
+echo BENCHES_OK
+# N = 2 rehearsal: two slab ranks sharing the one GPU (the N > 1 bench path)
+cd $R
+timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29702 bench.py --gpus 2 --rehearse-one-gpu --nx 2048 --rows-per-gpu 512 --stream-w 128 --steps 5 --warmup 1 2> $O/n2.err | grep '^{' > $O/bench_rehearse_n2.json || { tail -5 $O/n2.err; exit 1; }
+echo REHEARSE_OK
