@@ -430,12 +430,19 @@ struct PipeLds {
 // 6-wave workgroups then no longer fit one CU.
 extern __shared__ __attribute__((aligned(16))) unsigned char pipe_lds_image[];
 
+// Waves per SIMD the register allocation must leave room for: the narrow
+// W = 8 run kernel puts three 5-wave workgroups on a CU (4 waves on some
+// SIMDs: <= 128 VGPRs -- round 5's store-VGPR fix had pushed it to 132, and
+// eight slab processes sharing one GPU then no longer all fit)
+template <int W, bool SWEEP>
+constexpr int min_waves_of() { return (W == 8 && !SWEEP) ? 4 : 1; }
+
 // PAIR (W = 16 run kernel only): the tile's two
 // 8-column halves A (columns 0-7) and B (8-15) are marched by the same lanes,
 // B one step behind A, so every lane carries two independent cell chains per
 // diagonal -- each diagonal covers two columns, the launch half the diagonals.
 template <int W, bool SWEEP, bool PAIR = false>
-__global__ __launch_bounds__(threads_of<W>()) void pipe_kernel(PipeArgs a)
+__global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu(min_waves_of<W, SWEEP>()))) void pipe_kernel(PipeArgs a)
 {
     constexpr int kThreads = threads_of<W>();
     static_assert(win_of<W>() % uw_of<W>() == 0, "the window holds whole blocks");

@@ -15,3 +15,9 @@ for lib in cp2 cp2old; do
   run $lib 0 2048 512 16 4 || exit 1
   run $lib 1 2048 512 16 4 || exit 1
 done
+# the fixed default build's rates (compare: profiles/r05/ab/loaders, narrow/)
+for shp in "4096 4096 1" "16384 2048 10" "8192 8192 1" "1024 1024 1"; do
+  set -- $shp
+  timeout -k 10 150 python tools/probes/traj_rate.py $1 $2 $3 3 >> $O/rates.jsonl 2>> $O/err.log || exit 1
+done
+timeout -k 10 150 python tools/probes/sweep_rate.py 3 >> $O/rates.jsonl 2>> $O/err.log || exit 1
