@@ -95,8 +95,8 @@ constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, s
 constexpr int kR = kPipeR;
 constexpr unsigned G = kPipeGranuleStride;
 // BURG_DMA_READBACK: the loader reads each block's LDS-DMA bytes back before
-// it publishes filled[] (see the loader wave).  0 = rounds 2-4's protocol,
-// which races (A/B and race probe only).
+// it publishes filled[] (see the loader wave).  0 = rounds 2-4's protocol
+// (publish right after the covering vmcnt).
 #ifndef BURG_DMA_READBACK
 #define BURG_DMA_READBACK 1
 #endif
@@ -356,11 +356,12 @@ __device__ __forceinline__ void lds_st(LDS v4u *p, v4u v) { *(volatile lds_v4u *
 __device__ __forceinline__ unsigned lds_ld32(const LDS void *p) { return *(volatile const lds_u32 *)p; }
 __device__ __forceinline__ int lds_ldi(const LDS int *p) { return *(volatile const lds_i32 *)p; }
 __device__ __forceinline__ void lds_sti(LDS int *p, int v) { *(volatile lds_i32 *)p = v; }
-// Opaque copy of a store's offset: the store then reads exactly the VGPR the
-// caller keeps live afterwards (no immediate-offset folding, no in-place
-// offset increments); the data VGPRs are the kept values themselves -- see
-// the store VGPR note in the compute waves.
-__device__ __forceinline__ void launder(unsigned &off, v4u &) { asm volatile("" : "+v"(off)); }
+// Store VGPRs: a buffer store reads its offset and
+// data VGPRs after it issues, so the kernels keep them live until the next
+// iteration's stores.  launder: an opaque copy of a store's offset, so the
+// store reads exactly the VGPR that is kept (no immediate-offset folding, no
+// in-place offset increments); the data VGPRs are the kept values themselves.
+__device__ __forceinline__ void launder(unsigned &off) { asm volatile("" : "+v"(off)); }
 // (the comm wave: its data too -- a phi over two store branches let the
 // compiler keep a copy and reuse the stored registers)
 __device__ __forceinline__ void launder_all(unsigned &off, v4u &v) { asm volatile("" : "+v"(off), "+v"(v)); }
@@ -618,7 +619,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         long long t_prog = now_rt();
         unsigned long long iters = 0;
         // the previous iteration's sentinel stores (data, offsets), kept live
-        // until this one's (see keep_stores in the compute waves)
+        // until this one's (store VGPRs: see launder)
         v4u kc_s = v4u{0u, 0u, 0u, 0u}, kc_w = kc_s;
         unsigned kc_os = 0u, kc_ow = 0u;
         for (;;) {
@@ -947,7 +948,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         unsigned pwhy[5] = {0, 0, 0, 0, 0};
         bool paborted = false;
         // the previous paired diagonal's store data and offsets, kept live
-        // until this one's stores (see keep_stores in the one-cell kernel)
+        // until this one's stores (store VGPRs: see launder)
         v4u kq_a = v4u{0u, 0u, 0u, 0u}, kq_b = kq_a, kq_e = kq_a, kq_na = kq_a, kq_nb = kq_a;
         unsigned kq_ra = 0u, kq_rb = 0u, kq_eo = 0u, kq_oa = 0u, kq_ob = 0u;
         auto keep_prev = [&]() {
@@ -1082,8 +1083,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             keep_prev();
             unsigned ra = vA ? eA * 1024u + lane16 : kOOB, rb = vB ? eB * 1024u + lane16 : kOOB;
             v4u ka = outA, kb = outB;
-            launder(ra, ka);
-            launder(rb, kb);
+            launder(ra);
+            launder(rb);
             st_plain(ring, ra, ka);
             st_plain(ring, rb, kb);
             eA += atE ? 9u : 1u;
@@ -1095,7 +1096,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             unsigned eoff = kOOB;
             if (east_glob) {
                 eoff = out_e ? eb + (unsigned)((a.qbase + qB) & (kR - 1)) * (kWave * G) : kOOB;
-                launder(eoff, eo);
+                launder(eoff);
                 st_dev(wbox, eoff, eo);
             }
             unsigned offA = kOOB, offB = kOOB;
@@ -1110,8 +1111,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                            : kOOB;
                 kq_na = as_v4u(onA0, onA1);
                 kq_nb = as_v4u(onB0, onB1);
-                launder(offA, kq_na);
-                launder(offB, kq_nb);
+                launder(offA);
+                launder(offB);
                 st_sys(nrs, offA, kq_na);
                 st_sys(nrs, offB, kq_nb);
             }
@@ -1231,22 +1232,22 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 keep_prev();
                 unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u, rB = rA - 8192u;
                 v4u ka = outA, kb = outB;
-                launder(rA, ka);
-                launder(rB, kb);
+                launder(rA);
+                launder(rB);
                 st_plain(ring, rA, ka);
                 st_plain(ring, rB, kb);
                 v4u eo = as_v4u(oeB0, oeB1);
                 lds_st(atE ? eaddr : dumpv, eo);
                 unsigned eo_off = atE ? eoff : kOOB;
                 if (east_glob) {
-                    launder(eo_off, eo);
+                    launder(eo_off);
                     st_dev(wbox, eo_off, eo);
                 }
                 unsigned oa = (u < uw8 ? nA1 : nA2) + (unsigned)u * ncol;
                 unsigned ob = (u < uw8 ? nB1 : nB2) + (unsigned)u * ncol;
                 v4u na = as_v4u(onA0, onA1), nbv = as_v4u(onB0, onB1);
-                launder(oa, na);
-                launder(ob, nbv);
+                launder(oa);
+                launder(ob);
                 st_sys(nrs, oa, na);
                 st_sys(nrs, ob, nbv);
                 kq_a = ka;
@@ -1346,7 +1347,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
     // the previous diagonal's store data and offsets, kept live until this
-    // diagonal's stores (keep_stores below)
+    // diagonal's stores (store VGPRs: see launder)
     v4u kp_out = v4u{0u, 0u, 0u, 0u}, kp_e = kp_out, kp_n = kp_out;
     unsigned kp_ro = 0u, kp_eo = 0u, kp_no = 0u;
     unsigned long long spins = 0, slow_n = 0, ieee_n = 0, nonfin_n = 0, wait_ticks = 0;
@@ -1645,13 +1646,13 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         v4u outk = out;
         if constexpr (STEADY) {
             ro = lane16;
-            launder(ro, outk);
+            launder(ro);
             if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(outk, ring, ro, pw * 1024u, BURG_RING_AUX);
             else st_plain_so(ring, ro, pw * 1024u, outk);
             ++pw;  // (no wrap inside a steady block)
         } else {
             ro = valid ? pw * 1024u + lane16 : kOOB;
-            launder(ro, outk);
+            launder(ro);
             if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(outk, ring, ro, 0, BURG_RING_AUX);
             else st_plain(ring, ro, outk);
             pw = pw + 1 == Lu ? 0u : pw + 1;
@@ -1677,13 +1678,13 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             // two taken branches around a conditional one)
             if (WIDE || SE_G) {
                 eoff = atE ? se_eoff : kOOB;
-                launder(eoff, eo);
+                launder(eoff);
                 st_dev(wbox, eoff, eo);
             }
         }
         else if (EDGE && (WIDE || east_glob)) {
             eoff = east_glob && out_e ? eb + (unsigned)(aq & (kR - 1)) * (kWave * G) : kOOB;
-            launder(eoff, eo);
+            launder(eoff);
             st_dev(wbox, eoff, eo);
         }
         // (narrow steady blocks store unconditionally: nv1 / nv2 are out of
@@ -1697,18 +1698,18 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 // the top lane's slot: SGPR offset, advanced one column per diagonal
                 if constexpr (WIDE) {
                     noff = (has_north & (lane == top)) ? 0u : kOOB;
-                    launder(noff, no);
+                    launder(noff);
                     st_sys_so(nrs, noff, noffs, no);
                     noffs += ncol;
                 } else {
                     noff = (u < uwrap ? nv1 : nv2) + (unsigned)u * ncol;
-                    launder(noff, no);
+                    launder(noff);
                     st_sys(nrs, noff, no);
                 }
             } else {
                 noff = (out_n & (c < ncol_real)) ? nb + (unsigned)(aq & (kR - 1)) * nstep + (unsigned)c * ncol
                                                  : kOOB;
-                launder(noff, no);
+                launder(noff);
                 st_sys(nrs, noff, no);
             }
             kp_n = no;
