@@ -739,7 +739,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // published as soon as it (not the whole round) has landed.  (At a
         // priority above the compute waves' it would slow the compute wave it
         // shares a SIMD with, and with it the whole pipeline.)
-        __builtin_amdgcn_s_setprio(0);
+        // (BURG_LOADER_PRIO: race-screen builds only)
+#ifndef BURG_LOADER_PRIO
+#define BURG_LOADER_PRIO 0
+#endif
+        __builtin_amdgcn_s_setprio(BURG_LOADER_PRIO);
         // the compute waves run whole blocks of U diagonals
         const int total = (KW + kWave - 1 + U - 1) / U * U;
         const long long L = a.L;
@@ -861,7 +865,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     if (wave >= nval) return;
 
     // ================= compute wave =================
-    __builtin_amdgcn_s_setprio(1);
+    // (BURG_COMPUTE_PRIO: race-screen builds only)
+#ifndef BURG_COMPUTE_PRIO
+#define BURG_COMPUTE_PRIO 1
+#endif
+    __builtin_amdgcn_s_setprio(BURG_COMPUTE_PRIO);
     const int k = wave;
     const int tj = tj0 + k;
     const int tile = ti * ntj + tj;
