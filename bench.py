@@ -411,6 +411,38 @@ def _lib_source_id():
     return _lib.source_id()
 
 
+def _lib_build_flags():
+    from finitedifference_amd import _lib
+    return _lib.build_flags()
+
+
+HALO_MODES = {0: None, 1: "pinned host memory", 2: "consumer GPU memory over IPC (xGMI)"}
+
+
+def rank_diag(ctx, st, rank, kern_ms, launches, snap_every):
+    """What one rank of an N > 1 line saw: its kernel
+    time, the launch's ramp (first workgroup entry -> the last compute wave's
+    first block) and the wait for the rank below (-> the halo strip's first
+    block), south-inflow waits at the slab boundary (the halo ring) against
+    the in-GPU strip boundaries, the halo placement of both boundaries and why
+    a device ring was not used, the resolved snap_every, and the bounds-guard
+    counters (DESIGN.md sections 6.1, 7)."""
+    hin, hout = ctx.halo_modes()
+    return {"rank": rank,
+            "kernel_ms_last": round(st["loop_ms"], 3),
+            "kernel_ms_avg": round(kern_ms / max(launches, 1), 3),
+            "ramp_ms": round(st["ramp_ms"], 3),
+            "halo_wait_ms": round(st["halo_wait_ms"], 3),
+            "south_waits_halo": st["south_waits_halo"],
+            "south_wait_ms_halo": round(st["south_wait_ms_halo"], 3),
+            "south_waits_local": st["south_waits_local"],
+            "south_wait_ms_local": round(st["south_wait_ms_local"], 3),
+            "halo_in": HALO_MODES[hin], "halo_out": HALO_MODES[hout],
+            "halo_note": ctx.halo_note(),
+            "snap_every": snap_every,
+            "bounds_guard": {"checks": st["bounds_checks"], "hits": st["bounds_hits"]}}
+
+
 def main():
     args = parse()
     rank, world, local = dist_env()
@@ -554,13 +586,15 @@ def main():
 
     st_main = st
     halo = None
+    per_rank = None
     if world > 1:
         hin, hout = ctx.halo_modes()
-        halo = {0: None, 1: "pinned host memory", 2: "consumer GPU memory over IPC (xGMI)"}[
-            hout if rank == 0 else hin]
+        halo = HALO_MODES[hout if rank == 0 else hin]
         note = ctx.halo_note()
         if note:
             halo += f" ({note})"
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, rank_diag(ctx, st, rank, kern_ms, launches, ret_stride))
     ctx.close()  # give the trajectory ring back before the secondary probes
     if rank == 0:
         st = st_main
@@ -613,11 +647,17 @@ def main():
                 "halo_fallback": halo_fallback,
             },
             "residual_check": check,
-            "build_id": {"library": _lib_build_id(), "sources": _lib_source_id()},
+            "build_id": {"library": _lib_build_id(), "sources": _lib_source_id(),
+                         "flags": _lib_build_flags()},
             "engine": {"name": eng, "tile_w": st["stream_w"], "tiles": st["stream_tiles"],
                        "blocked_diagonals": st["slow_diagonals"],
                        "spin_polls": st["stall_spins"], "ieee_diagonals": st["ieee_diagonals"],
-                       "comm_polls": st["comm_polls"]},
+                       "comm_polls": st["comm_polls"], "ramp_ms": round(st["ramp_ms"], 3),
+                       "bounds_guard": {"checks": st["bounds_checks"], "hits": st["bounds_hits"],
+                                        "what": "copy calls of this context that checked the "
+                                                "ring/transpose kernels' bounds guard (err[5], "
+                                                "DESIGN.md section 6.1), and hits (each one "
+                                                "fails its call)"}},
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
@@ -629,6 +669,8 @@ def main():
                 "traffic_source": tsrc,
             },
         }
+        if per_rank is not None:
+            out["per_rank"] = per_rank
         if alone is not None:
             out["per_gpu_alone"] = alone
             out["weak_eff_same_shape"] = round(value / (world * alone["value"]), 4)
@@ -641,6 +683,7 @@ def main():
                 out["issue_roofline"] = iss
         if world == 1 and not args.no_1024:
             out["config2_1024"] = config2_1024(args.pmc_file, args.isa_file)
+            out["single_1024"] = single_1024(args.pmc_file, args.isa_file)
         if world == 1 and not args.no_e2e:
             out["end_to_end"] = end_to_end()
         if world == 1 and args.stencil_nx > 0:
@@ -723,6 +766,59 @@ def residual_check(ctx, T, dist=None, device=None, snap_every=1):
                     "rows from the rank below",
             "rel": rel, "max_over_ranks_slab_rel": srel, "norm_R_T": n1, "norm_R_T-1": n0,
             "tol": RESIDUAL_TOL, "ok": bool(rel < RESIDUAL_TOL and srel < RESIDUAL_TOL)}
+
+
+def single_1024(pmc_file, isa_file=None, steps=5):
+    """run_fom.main's own unit at BASELINE configs[1]: ONE 1024^2 x 500
+    trajectory (dt = 0.05, mu = (5.19, 0.026), w0 = 1) in one burg_trajectory
+    launch, every state kept in HBM -- priced against the HBM roofline (32 B
+    per cell-update), against its PMC traffic and against the compute waves'
+    issue floor; secondary to the headline."""
+    from finitedifference_amd.solver import FOMContext
+    nx, T = 1024, 500
+    ctx = FOMContext(nx, nx, engine="pipe")
+    g = np.linspace(0, 100, nx + 1)
+    ctx.set_problem(g, g, DT, MU)
+    ctx.upload(np.ones(ctx.m))
+    ctx.reserve(T)
+    ctx.trajectory(T)
+    t0 = time.perf_counter()
+    kern = 0.0
+    for _ in range(steps):
+        st = ctx.trajectory(T)
+        kern += st["loop_ms"]
+    el = time.perf_counter() - t0
+    ctx.close()
+    upd = nx * nx * T
+    ms = kern / steps
+    gbs = BYTES_PER_CELL_UPDATE * upd / (ms * 1e-3) / 1e9
+    key = f"pipe:{nx}x{nx}:T{T}"
+    traffic, tsrc = read_pmc(pmc_file, key)
+    clk, csrc = read_clock(pmc_file, key)
+    paired = st.get("paired_launches", 0) > 0
+    W = st["stream_w"]
+    if paired:
+        kname = f"pipe_kernel<{W}, false, paired (per cell)>"
+        cell_diags = 2 * (T * W // 2 + 2 * nx)
+    else:
+        kname = f"pipe_kernel<{W}, false>"
+        cell_diags = T * W + 2 * nx
+    iss = issue_roofline(kname, ms, cell_diags, isa_file, W, U=block_of(W), clock_ghz=clk,
+                         clock_src=csrc) if isa_file else None
+    meas = (round(traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+            if isinstance(traffic, (int, float)) and traffic > 0 else None)
+    return {"grid": f"{nx}x{nx}", "dt": DT, "unit_of_work": f"one trajectory x {T} steps "
+                                                          "(run_fom.main's loop)",
+            "value": round(upd * steps / el / 1e6, 3), "unit": "Mcell-updates/s",
+            "kernel": kname, "tile_w": W, "tiles": st["stream_tiles"],
+            "avg_launch_ms": round(ms, 4), "ramp_ms": round(st["ramp_ms"], 3),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 5),
+                         "per_launch_alg_bytes": BYTES_PER_CELL_UPDATE * upd,
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "frac_measured_traffic": meas},
+            "issue_roofline": iss, "paired_halves": paired,
+            "ieee_diagonals": st["ieee_diagonals"]}
 
 
 def config2_1024(pmc_file, isa_file=None, steps=3):

@@ -13,7 +13,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libburgers_hip.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 BURG_OK, BURG_EINVAL, BURG_ESHAPE, BURG_EHIP, BURG_EHALO = 0, -1, -2, -3, -4
 BURG_ENOMEM, BURG_ENOCONV, BURG_ENAN, BURG_ESTATE = -5, -6, -7, -8
@@ -30,7 +30,8 @@ EXPORTS = (
     "burg_trajectory_plan", "burg_trajectory_retained", "burg_trajectory_copy",
     "burg_sweep_device", "burg_pod_rsvd_device",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
-    "burg_pod", "burg_pod_rsvd", "burg_run_npy", "burg_build_id", "burg_ring_audit",
+    "burg_pod", "burg_pod_rsvd", "burg_run_npy", "burg_run_npy_ex", "burg_build_id",
+    "burg_build_flags", "burg_ring_audit",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -63,6 +64,14 @@ class BurgStats(ctypes.Structure):
         ("comm_polls", ctypes.c_int64),
         ("nonfinite_diagonals", ctypes.c_int64),
         ("paired_launches", ctypes.c_int64),
+        ("ramp_ms", ctypes.c_double),
+        ("halo_wait_ms", ctypes.c_double),
+        ("south_waits_local", ctypes.c_int64),
+        ("south_waits_halo", ctypes.c_int64),
+        ("south_wait_ms_local", ctypes.c_double),
+        ("south_wait_ms_halo", ctypes.c_double),
+        ("bounds_checks", ctypes.c_int64),
+        ("bounds_hits", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -171,6 +180,10 @@ def load(path=None):
                                              _D]),
             "burg_run_npy": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                             ctypes.POINTER(BurgStats)]),
+            "burg_run_npy_ex": (ctypes.c_int, [_VP, _D, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_char_p, ctypes.c_int,
+                                               ctypes.POINTER(BurgStats)]),
+            "burg_build_flags": (ctypes.c_char_p, []),
             "burg_sweep": (ctypes.c_int, [_VP, ctypes.c_int, _D, _D, ctypes.c_int,
                                           ctypes.POINTER(_D), ctypes.c_int64, ctypes.c_int,
                                           ctypes.POINTER(BurgStats)]),
@@ -216,6 +229,17 @@ def source_id(csrc=_CSRC):
 def build_id():
     """burg_build_id() of the loaded library."""
     return load().burg_build_id().decode()
+
+
+def build_flags():
+    """burg_build_flags() of the loaded library: 'HIPFLAGS | knobs: ...'
+    ('knobs: none' for the default build; A/B and race-screen variants name
+    their -D knobs, csrc/Makefile VARIANT / KNOBS)."""
+    return load().burg_build_flags().decode()
+
+
+def is_default_build():
+    return build_flags().endswith("knobs: none")
 
 
 def ring_audit(W, num_steps, snap_every=1, ring_cap=0):

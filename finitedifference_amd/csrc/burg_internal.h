@@ -76,6 +76,13 @@ struct StreamStats {
     unsigned long long prof[8];  // pipe, built with -DBURG_PIPE_PROF: compute-wave clocks in
                                  // [0] the loop, [1] block-start store waits, [2] readiness
                                  // waits, [4 + k] readiness waits of compute wave k
+    // pipe launch diagnostics (s_memrealtime, 100 MHz; reset before every
+    // launch, stream_launch): first workgroup entry (min), the latest compute
+    // wave's first block (max), the halo strip's earliest first block (min;
+    // ~0: no inbound halo); blocks that waited for south inflow and their
+    // waiting time, [0] from a strip of this GPU, [1] from the halo ring
+    unsigned long long t_entry, t_halo_first, t_first_max;
+    unsigned long long south_blocks[2], south_rt[2];
 };
 
 // Tiling of a slab for the streaming engine: nti strips of 64 rows, ntj tiles
@@ -155,6 +162,17 @@ struct RetCursor {
         return e;
     }
 };
+
+// The diagnosis words err[1..3] of a failed wait (tile, diagonal, kind), as
+// three separate 32-bit stores: merged into one dwordx3 store the compiler
+// would reuse its data VGPRs a few instructions later (the store-VGPR rule
+// of DESIGN.md section 6.2 -- tools/store_reuse_check.py)
+__device__ inline void set_err3(unsigned *err, unsigned tile, unsigned where, unsigned kind)
+{
+    *(volatile unsigned *)&err[1] = tile;
+    *(volatile unsigned *)&err[2] = where;
+    *(volatile unsigned *)&err[3] = kind;
+}
 
 struct StreamArgs {
     Coeffs cf;

@@ -21,11 +21,12 @@
 
 #include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 #include "../../include/burgers.h"
 #include "burg_internal.h"
-#include "build/build_id.h"
+#include "build_id.h"  // (the object directory's, -I$(B): Makefile)
 
 using namespace burg;
 
@@ -197,6 +198,9 @@ struct burg_ctx {
                                      // overwrites it)
     bool halo_out_resolved = false;  // producer: took the consumer's verdict (first launch)
     std::string halo_note;           // why a device ring was not used
+    // the last pipe launch's diagnostics (burg_stats ramp_ms / halo_wait_ms)
+    double last_ramp_ms = 0.0, last_halo_wait_ms = -1.0;
+    int64_t bounds_checks = 0, bounds_hits = 0;  // check_bounds calls / hits (lifetime)
 
     size_t m() const { return 2 * (size_t)nx * nrows; }
     size_t n() const { return (size_t)nx * nrows; }
@@ -395,7 +399,9 @@ int check_bounds(burg_ctx *c, const char *where)
     unsigned f = 0;
     HIPCHK(hipMemcpyAsync(&f, c->d_err + 5, sizeof f, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    ++c->bounds_checks;
     if (!f) return 0;
+    ++c->bounds_hits;
     (void)hipMemsetAsync(c->d_err + 5, 0, sizeof f, c->stream);
     (void)hipStreamSynchronize(c->stream);
     return fail(BURG_EHIP, "%s: internal bounds check failed (%s%s): a library bug -- please "
@@ -686,6 +692,12 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
             if (!ok && c->world > 1) c->slab_failed = true;
         }
     } guard{c};
+    if (pipe) {
+        // the launch diagnostics' timers: t_entry, t_halo_first start at ~0
+        // (atomicMin), t_first_max at 0 (atomicMax)
+        HIPCHK(hipMemsetAsync(&c->d_sstats->t_entry, 0xFF, 2 * sizeof(unsigned long long), c->stream));
+        HIPCHK(hipMemsetAsync(&c->d_sstats->t_first_max, 0, sizeof(unsigned long long), c->stream));
+    }
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
         const PipeArgs pa = pipe_args(c, L, origin, K, mp);
@@ -725,7 +737,9 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
                         "pipe engine: a wait timed out (workgroup tile %u of %d, step/diagonal %u, "
                         "wait %#x [16: comm wave: 1 south 2 west 4 north-grant 8 east-grant; 32: "
                         "compute wave, missing (>> 8): 1 west 2 south 4 east-LDS 8 east-grant "
-                        "16 north-grant 32 state window; 128: loader], K=%d W=%d%s)",
+                        "16 north-grant 32 state window; 128: loader, >> 8 which one -- tile = "
+                        "its first compute wave's, step = that wave's filled diagonals], "
+                        "K=%d W=%d%s)",
                         err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W,
                         c->world > 1 ? "; multi-GPU: a neighbour rank may not be running" : "");
         return fail(BURG_EHIP,
@@ -733,7 +747,16 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
                     "edges %u [1 west 2 south 4 east 8 north], K=%d W=%d)",
                     err[1], c->sp.ntiles, err[2], err[3], K, c->sp.W);
     }
-    if (pipe) c->qbase = (int)((c->qbase + (long long)K) % (2 * kPipeR));
+    if (pipe) {
+        c->qbase = (int)((c->qbase + (long long)K) % (2 * kPipeR));
+        unsigned long long tm[3] = {0, 0, 0};  // t_entry, t_halo_first, t_first_max
+        HIPCHK(hipMemcpy(tm, &c->d_sstats->t_entry, sizeof tm, hipMemcpyDeviceToHost));
+        const unsigned long long none = ~0ull;
+        c->last_ramp_ms = (tm[0] != none && tm[2] >= tm[0]) ? (double)(tm[2] - tm[0]) / 1e5 : 0.0;
+        c->last_halo_wait_ms = (tm[0] != none && tm[1] != none && tm[1] >= tm[0])
+                                   ? (double)(tm[1] - tm[0]) / 1e5
+                                   : -1.0;
+    }
     guard.ok = true;
     return 0;
 }
@@ -786,6 +809,19 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
         st->comm_polls = c->eng_eff == BURG_ENGINE_PIPE ? (int64_t)ss.why[5] : 0;
         st->nonfinite_diagonals = (int64_t)ss.nonfinite_diagonals;
         st->paired_launches = c->paired_launches;
+        if (c->eng_eff == BURG_ENGINE_PIPE) {
+            // (s_memrealtime: 100 MHz)
+            st->ramp_ms = c->last_ramp_ms;
+            st->halo_wait_ms = c->last_halo_wait_ms;
+            st->south_waits_local = (int64_t)ss.south_blocks[0];
+            st->south_waits_halo = (int64_t)ss.south_blocks[1];
+            st->south_wait_ms_local = (double)ss.south_rt[0] / 1e5;
+            st->south_wait_ms_halo = (double)ss.south_rt[1] / 1e5;
+        } else {
+            st->halo_wait_ms = -1.0;
+        }
+        st->bounds_checks = c->bounds_checks;
+        st->bounds_hits = c->bounds_hits;
     }
     if (ss.nonfinite_diagonals && !std::getenv("BURG_ALLOW_NONFINITE"))  // (diagnostics knob)
         return fail(BURG_ENAN,
@@ -2750,11 +2786,26 @@ static std::string npy_header(size_t m, size_t ncols)
 int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, const char *path,
                  burg_stats *st)
 {
+    return burg_run_npy_ex(c, w0, num_steps, snap_every, path, 0, st);
+}
+
+// burg_run_npy_ex: the same, with BURG_NPY_GLOBAL -- a slab context writes
+// its rows at their places in the WHOLE grid's (2 nx ny_total, ncols) matrix:
+// its u rows at global rows row0 nx ..., its v rows at nx ny_total + row0 nx
+// ... (the reference layout, C/hypernet2D.py:89-90,126; SURVEY.md 8(e): "each
+// GPU copies its slab rows directly into the right rows") -- and
+// BURG_NPY_EXISTING -- the file exists already, made by one rank with the
+// whole matrix's header and size (checked here), and is neither truncated nor
+// given a header, so every rank of a job writes into the same file at once.
+int burg_run_npy_ex(burg_ctx *c, const double *w0, int num_steps, int snap_every, const char *path,
+                    int flags, burg_stats *st)
+{
     BURG_TRACE("burg_run_npy");
     if (int e = check_ready(c)) return e;
     if (st) std::memset(st, 0, sizeof *st);
     if (!w0 || !path || !*path) return fail(BURG_EINVAL, "null w0 or path");
     if (num_steps < 1 || snap_every < 1) return fail(BURG_EINVAL, "num_steps, snap_every >= 1");
+    if (flags & ~(BURG_NPY_GLOBAL | BURG_NPY_EXISTING)) return fail(BURG_EINVAL, "unknown flags %#x", flags);
     if (c->engine == BURG_ENGINE_TILES) return fail(BURG_EINVAL, "burg_run_npy runs on the stream/pipe engines");
     if (int e = stream_setup(c)) return e;
     if (num_steps > stream_max_steps(c))
@@ -2762,6 +2813,14 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
     const int W = c->sp.W;
     const size_t m = c->m();
     const int64_t ncols = num_steps / snap_every + 1;
+    // the file's matrix and where this context's rows go: local row e < n is
+    // u row e, at file row urow0 + e; e >= n at vrow0 + e - n
+    const bool global = (flags & BURG_NPY_GLOBAL) != 0;
+    const size_t nloc = c->n();
+    const size_t n_file = global ? (size_t)c->nx * c->ny_total : nloc;
+    const size_t m_file = 2 * n_file;
+    const size_t urow0 = global ? (size_t)c->row0 * c->nx : 0;
+    const size_t vrow0 = n_file + urow0;
     const long long L = (long long)num_steps * W + W + 96;
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     size_t freeb = 0, totalb = 0;
@@ -2825,15 +2884,35 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         }
         free_buf.push_back(i);
     }
-    fd = open(path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
-    if (fd < 0) {
-        cleanup();
-        return fail(BURG_EINVAL, "open(%s): %s", path, strerror(errno));
-    }
-    const std::string hdr = npy_header(m, (size_t)ncols);
-    if (write(fd, hdr.data(), hdr.size()) != (ssize_t)hdr.size()) {
-        cleanup();
-        return fail(BURG_EINVAL, "write(%s): %s", path, strerror(errno));
+    const std::string hdr = npy_header(m_file, (size_t)ncols);
+    const off_t file_bytes = (off_t)(hdr.size() + m_file * row_bytes);
+    if (flags & BURG_NPY_EXISTING) {
+        // another rank made the file: it must already be this matrix's
+        fd = open(path, O_RDWR);
+        if (fd < 0) {
+            cleanup();
+            return fail(BURG_EINVAL, "open(%s): %s", path, strerror(errno));
+        }
+        std::string got(hdr.size(), '\0');
+        struct stat sb {};
+        if (pread(fd, &got[0], got.size(), 0) != (ssize_t)got.size() || got != hdr ||
+            fstat(fd, &sb) != 0 || sb.st_size < file_bytes) {
+            cleanup();
+            return fail(BURG_EINVAL, "%s is not a (%zu, %lld) float64 .npy of %lld bytes made for this "
+                        "trajectory (BURG_NPY_EXISTING)", path, m_file, (long long)ncols,
+                        (long long)file_bytes);
+        }
+    } else {
+        fd = open(path, O_CREAT | O_TRUNC | O_WRONLY, 0644);
+        if (fd < 0) {
+            cleanup();
+            return fail(BURG_EINVAL, "open(%s): %s", path, strerror(errno));
+        }
+        if (write(fd, hdr.data(), hdr.size()) != (ssize_t)hdr.size() ||
+            (global && ftruncate(fd, file_bytes) != 0)) {
+            cleanup();
+            return fail(BURG_EINVAL, "write(%s): %s", path, strerror(errno));
+        }
     }
     for (int w = 0; w < NW; ++w)
         writers.emplace_back([&]() {
@@ -2886,9 +2965,26 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
     hipEvent_t f0 = nullptr, f1 = nullptr;
     (void)hipEventCreate(&f0);
     (void)hipEventCreate(&f1);
+    // a buffer taken off free_buf goes back on every failure path, so the
+    // drain below (every buffer free again) always ends
+    auto give_back = [&](int b) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            free_buf.push_back(b);
+        }
+        cv.notify_all();
+    };
+    // test knob: the copy of row block BURG_TEST_FAIL_NPY_BLOCK (0-based)
+    // fails as a faulted gather or D2H would (tests/test_gpu_parity.py)
+    long long fail_blk = -1;
+    if (const char *e = std::getenv("BURG_TEST_FAIL_NPY_BLOCK")) fail_blk = std::atoll(e);
     int di = 0;  // device gather buffer (two, alternating)
-    for (size_t e0 = 0; e0 < m && rc == BURG_OK; e0 += R, di ^= 1) {
-        const size_t ne = std::min(R, m - e0);
+    long long blk = 0;
+    // (a block stays inside the u rows or inside the v rows: the two land in
+    // different places of a global file)
+    for (size_t e0 = 0, ne = 0; e0 < m && rc == BURG_OK; e0 += ne, di ^= 1, ++blk) {
+        ne = std::min(R, (e0 < nloc ? nloc : m) - e0);
+        const size_t frow = e0 < nloc ? urow0 + e0 : vrow0 + (e0 - nloc);
         int b = -1;
         {
             std::unique_lock<std::mutex> g(mu);
@@ -2899,15 +2995,18 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         }
         double *dst = d_blk + (size_t)di * R * ncols;
         (void)hipEventRecord(f0, c->stream);
-        if (launch_ring_extract_rows(stream_args(c, L, 0, 0), W, e0, ne, 0, snap_every, (int)ncols,
+        if (blk == fail_blk ||
+            launch_ring_extract_rows(stream_args(c, L, 0, 0), W, e0, ne, 0, snap_every, (int)ncols,
                                      dst, R * (size_t)ncols, c->stream) ||
             hipMemcpyAsync(h_blk[b], dst, ne * row_bytes, hipMemcpyDeviceToHost, c->stream) !=
                 hipSuccess) {
-            rc = fail(BURG_EHIP, "snapshot row block copy failed");
+            give_back(b);
+            rc = fail(BURG_EHIP, "snapshot row block copy failed (rows %zu..%zu)", e0, e0 + ne);
             break;
         }
         (void)hipEventRecord(f1, c->stream);
         if (hipEventSynchronize(f1) != hipSuccess) {
+            give_back(b);
             rc = fail(BURG_EHIP, "snapshot row block copy failed: %s", hipGetErrorString(hipGetLastError()));
             break;
         }
@@ -2916,7 +3015,7 @@ int burg_run_npy(burg_ctx *c, const double *w0, int num_steps, int snap_every, c
         flush_ms += t;
         {
             std::lock_guard<std::mutex> g(mu);
-            jobs.push_back({b, (off_t)(hdr.size() + e0 * row_bytes), ne * row_bytes});
+            jobs.push_back({b, (off_t)(hdr.size() + frow * row_bytes), ne * row_bytes});
         }
         cv.notify_all();
     }
@@ -3300,6 +3399,7 @@ static int pod_impl(int device, int64_t m, int ns, const double *snaps, bool sna
 }
 
 const char *burg_build_id(void) { return BURG_BUILD_ID; }
+const char *burg_build_flags(void) { return BURG_BUILD_FLAGS; }
 
 // Host-only replay of every ring entry the pipe engine's trajectory kernels
 // form (include/burgers.h).  The walks below are the

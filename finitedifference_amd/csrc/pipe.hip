@@ -339,6 +339,21 @@ __device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballo
 
 // (RetCursor, the retained-window walk: burg_internal.h)
 
+// Launch diagnostics of one compute wave (lane 0, once, at its end;
+// DESIGN.md section 7): when its first block could start (the latest over
+// the launch = the ramp; the earliest over the slab's halo strip = the wait
+// for the rank below), and its blocks that waited for south inflow, split by
+// where that inflow comes from (the halo ring / a strip of this GPU).
+__device__ __forceinline__ void launch_diag(const PipeArgs &a, bool halo, long long first,
+                                            unsigned south_blocks, unsigned long long south_rt)
+{
+    atomicMax(&a.stats->t_first_max, (unsigned long long)first);
+    if (halo) atomicMin(&a.stats->t_halo_first, (unsigned long long)first);
+    const int h = halo ? 1 : 0;
+    if (south_blocks) atomicAdd(&a.stats->south_blocks[h], (unsigned long long)south_blocks);
+    if (south_rt) atomicAdd(&a.stats->south_rt[h], south_rt);
+}
+
 
 // LDS accesses that must not be cached in registers or merged (polled / handed
 // off between waves).  Explicit address space 3: a volatile access through a
@@ -506,6 +521,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         if (__hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
             ok = 0;
         } else {
+            // (launch diagnostics: the first workgroup's entry)
+            atomicMin(&a.stats->t_entry, (unsigned long long)now_rt());
             atomicAdd(a.census, 1u);
             const long long t0 = now_rt();
             for (;;) {
@@ -518,9 +535,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 }
                 if (now_rt() - t0 > a.census_ticks) {
                     if (atomicOr(a.err, 1u) == 0) {
-                        a.err[1] = (unsigned)wg;
-                        a.err[2] = n;
-                        a.err[3] = 64u;
+                        set_err3(a.err, (unsigned)wg, n, 64u);
                     }
                     ok = 0;
                     break;
@@ -709,11 +724,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 if (lane == 0) {
                     lds_sti(&sm.perm[5], 1);
                     if (atomicOr(a.err, 1u) == 0) {
-                        a.err[1] = (unsigned)(ti * ntj + tj0);
-                        a.err[2] = (unsigned)min(min(wS ? qs : INT_MAX, wN ? qn : INT_MAX),
-                                                 min(wW ? qw : INT_MAX, wE ? qe : INT_MAX));
-                        a.err[3] = 16u | (__any(wS) ? 1u : 0u) | (__any(wW) ? 2u : 0u) |
-                                   (__any(wN) ? 4u : 0u) | (__any(wE) ? 8u : 0u);
+                        set_err3(a.err, (unsigned)(ti * ntj + tj0),
+                                 (unsigned)min(min(wS ? qs : INT_MAX, wN ? qn : INT_MAX),
+                                               min(wW ? qw : INT_MAX, wE ? qe : INT_MAX)),
+                                 16u | (__any(wS) ? 1u : 0u) | (__any(wW) ? 2u : 0u) |
+                                     (__any(wN) ? 4u : 0u) | (__any(wE) ? 8u : 0u));
                     }
                 }
                 break;
@@ -850,9 +865,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                     if (lane == 0 && !lds_ldi(&sm.perm[5])) {
                         lds_sti(&sm.perm[5], 1);
                         if (atomicOr(a.err, 1u) == 0) {
-                            a.err[1] = (unsigned)(ti * ntj + tj0);
-                            a.err[2] = (unsigned)nf[0];
-                            a.err[3] = 128u;
+                            // (the first compute wave this loader fills, and
+                            // the loader's index in err[3] >> 8: ADVICE r05)
+                            const int k0 = lw * 4 / nl_of<W>();
+                            set_err3(a.err, (unsigned)(ti * ntj + tj0 + k0), (unsigned)nf[k0],
+                                     128u | ((unsigned)lw << 8));
                         }
                     }
                     break;
@@ -1274,12 +1291,16 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             if (eA >= Lu) eA -= Lu;
         };
         __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
+        // launch diagnostics: when the wave's first block could start, and
+        // the time its blocks waited for south inflow (s_memrealtime)
+        long long p_first = now_rt();
+        unsigned long long p_srt = 0;
         for (int sb = 0; sb < total2; sb += U) {
             lds_sti(lane == 0 ? &sm.prog[k] : sink, sb);
             if (__builtin_expect(missing2(sb, false) != 0, 0)) {
                 long long t0 = 0;
                 unsigned long long c0 = 0;
-                bool waited = false;
+                bool waited = false, wsouth = false;
                 for (;;) {
                     const unsigned why = missing2(sb, true);
                     if (!why) break;
@@ -1292,13 +1313,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                         pwhy[1] += (why & 16u) != 0;
                         pwhy[2] += (why & 1u) != 0;
                         pwhy[3] += (why & 2u) != 0;
+                        wsouth = (why & 2u) != 0;
                     } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                         if (lane == 0 && !lds_ldi(&sm.perm[5])) {
                             lds_sti(&sm.perm[5], 1);
                             if (atomicOr(a.err, 1u) == 0) {
-                                a.err[1] = (unsigned)tile;
-                                a.err[2] = (unsigned)sb;
-                                a.err[3] = 32u | (why << 8);
+                                set_err3(a.err, (unsigned)tile, (unsigned)sb, 32u | (why << 8));
                             }
                         }
                         paborted = true;
@@ -1307,7 +1327,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                     ++pspins;
                     __builtin_amdgcn_s_sleep(1);
                 }
-                if (waited) pwait += __builtin_amdgcn_s_memtime() - c0;
+                if (waited) {
+                    pwait += __builtin_amdgcn_s_memtime() - c0;
+                    const long long tw = now_rt();
+                    if (sb == 0) p_first = tw;
+                    if (wsouth) p_srt += (unsigned long long)(tw - t0);
+                }
                 if (paborted) break;
             }
             bool steady = (a.pair == 1) & (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
@@ -1348,6 +1373,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             if (pwait) atomicAdd(&a.stats->slow_ticks, pwait);
             for (int i = 0; i < 5; ++i)
                 if (pwhy[i]) atomicAdd(&a.stats->why[i], (unsigned long long)pwhy[i]);
+            launch_diag(a, south_host, p_first, pwhy[3], p_srt);
             atomicAdd(&a.stats->tile_steps, (unsigned long long)K);
         }
         return;
@@ -1829,6 +1855,10 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     unsigned long long pf_vm = 0;
     const unsigned long long pf0 = __builtin_amdgcn_s_memtime();
 #endif
+    // launch diagnostics: when the wave's first block could start, and the
+    // time its blocks waited for south inflow (s_memrealtime)
+    long long d_first = now_rt();
+    unsigned long long d_srt = 0;
     for (int sb = 0; sb < total; sb += U) {
 #ifdef BURG_PIPE_PROF
         const unsigned long long pfa = __builtin_amdgcn_s_memtime();
@@ -1851,7 +1881,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             // (block_missing runs inside the wait loop, out of the hot path)
             long long t0 = 0;
             unsigned long long c0 = 0;
-            bool waited = false;
+            bool waited = false, wsouth = false;
             for (;;) {
                 const unsigned why = block_missing(sb);
                 if (!why) break;
@@ -1865,13 +1895,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                     wait_why[2] += (why & 1u) != 0;   // west inflow
                     wait_why[3] += (why & 2u) != 0;   // south inflow
                     wait_why[4] += (why & 32u) != 0;  // previous states (loader window)
+                    wsouth = (why & 2u) != 0;
                 } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                     if (lane == 0 && !lds_ldi(&sm.perm[5])) {
                         lds_sti(&sm.perm[5], 1);
                         if (atomicOr(a.err, 1u) == 0) {
-                            a.err[1] = (unsigned)tile;
-                            a.err[2] = (unsigned)sb;
-                            a.err[3] = 32u | (why << 8);
+                            set_err3(a.err, (unsigned)tile, (unsigned)sb, 32u | (why << 8));
                         }
                     }
                     aborted = true;
@@ -1880,7 +1909,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 ++spins;
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (waited) wait_ticks += __builtin_amdgcn_s_memtime() - c0;
+            if (waited) {
+                wait_ticks += __builtin_amdgcn_s_memtime() - c0;
+                const long long tw = now_rt();
+                if (sb == 0) d_first = tw;
+                if (wsouth) d_srt += (unsigned long long)(tw - t0);
+            }
             if (aborted) break;
         }
         // (retained windows: the block's ring entries are consecutive and
@@ -1943,6 +1977,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         if (wait_ticks) atomicAdd(&a.stats->slow_ticks, wait_ticks);
         for (int i = 0; i < 5; ++i)
             if (wait_why[i]) atomicAdd(&a.stats->why[i], (unsigned long long)wait_why[i]);
+        launch_diag(a, south_host, d_first, wait_why[3], d_srt);
 #ifdef BURG_PIPE_PROF
         atomicAdd(&a.stats->prof[0], __builtin_amdgcn_s_memtime() - pf0);
         atomicAdd(&a.stats->prof[1], pf_vm);

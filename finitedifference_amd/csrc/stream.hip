@@ -105,6 +105,15 @@ __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off
 template <int W>
 constexpr int ilog2() { return W <= 1 ? 0 : 1 + ilog2<W / 2>(); }
 
+// Store VGPRs (as pipe.hip): an opaque copy of a
+// store's offset, so the store reads exactly the VGPR the kernel keeps live
+// until the next diagonal's stores (tools/store_reuse_check.py checks it)
+__device__ __forceinline__ unsigned launder(unsigned off)
+{
+    asm volatile("" : "+v"(off));
+    return off;
+}
+
 // One wavefront per tile; 4 tiles per workgroup (one per SIMD).
 template <int W, int D, int DM>
 __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
@@ -238,6 +247,10 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
     __builtin_amdgcn_s_waitcnt(0);
 
     double e0 = 0.0, e1 = 0.0, no0 = 0.0, no1 = 0.0;
+    // the previous diagonal's store data and offsets, kept live until this
+    // diagonal's stores (store VGPRs)
+    v4u k_out = v4u{0u, 0u, 0u, 0u}, k_e = k_out, k_n = k_out;
+    unsigned k_r = 0u, k_w0 = 0u, k_we = 0u, k_s0 = 0u, k_sn = 0u;
     unsigned spins = 0, slow_n = 0, nonfin_n = 0, why_n[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long slow_t = 0;
     bool bad_range = false;
@@ -316,9 +329,7 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
                     if (has_east && __any(valid && rowok && atE && !all_sent(gw[m]))) why |= 4;
                     if (has_north && __any(valid && n_out && !all_sent(gs[m]))) why |= 8;
                     if (lane == 0 && atomicOr(a.err, 1u) == 0) {
-                        a.err[1] = tile;
-                        a.err[2] = s;
-                        a.err[3] = why;
+                        set_err3(a.err, (unsigned)tile, (unsigned)s, why);
                     }
                     break;
                 }
@@ -352,11 +363,25 @@ __global__ __launch_bounds__(256) void stream_kernel(StreamArgs a)
         if constexpr (LDSST) {
             if (t >= 0) *st_slot = out;
         }
-        st_plain(ring, valid ? (unsigned)pw * 1024u + lane16 : kOOB, out);
-        st_sc1(wbox, at0 ? ow[m] : kOOB, sent);               // consumed: empty it
-        st_sc1(wbox, atE ? ow[m] : kOOB, as_v4u(oe0, oe1));   // east outflow
-        st_sc1(sbox, s_in ? os[m] : kOOB, sent);
-        st_sc1(sbox, s_in ? kOOB : os[m], as_v4u(on0, on1));  // north outflow
+        asm volatile("" ::"v"(k_out), "v"(k_e), "v"(k_n), "v"(k_r), "v"(k_w0), "v"(k_we), "v"(k_s0),
+                     "v"(k_sn));
+        const v4u eo = as_v4u(oe0, oe1), no = as_v4u(on0, on1);
+        const unsigned o_r = launder(valid ? (unsigned)pw * 1024u + lane16 : kOOB);
+        const unsigned o_w0 = launder(at0 ? ow[m] : kOOB), o_we = launder(atE ? ow[m] : kOOB);
+        const unsigned o_s0 = launder(s_in ? os[m] : kOOB), o_sn = launder(s_in ? kOOB : os[m]);
+        st_plain(ring, o_r, out);
+        st_sc1(wbox, o_w0, sent);  // consumed: empty it
+        st_sc1(wbox, o_we, eo);    // east outflow
+        st_sc1(sbox, o_s0, sent);
+        st_sc1(sbox, o_sn, no);    // north outflow
+        k_out = out;
+        k_e = eo;
+        k_n = no;
+        k_r = o_r;
+        k_w0 = o_w0;
+        k_we = o_we;
+        k_s0 = o_s0;
+        k_sn = o_sn;
         pw = pw + 1 == L ? 0 : pw + 1;
         prefetch_ring(s + D, k);
         prefetch_mail(s + DM, m);

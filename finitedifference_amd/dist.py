@@ -16,10 +16,11 @@ reference layout.
 """
 import os
 import secrets
+import tempfile
 
 import numpy as np
 
-from .solver import FOMContext
+from .solver import NPY_EXISTING, NPY_GLOBAL, FOMContext
 
 
 def slab_rows(ny, world, rank):
@@ -150,3 +151,133 @@ def slab_residual_norms(ctx, w, wp, dist=None, device=None):
     t = torch.tensor([ss], dtype=torch.float64, device=dev)
     dist.all_reduce(t)
     return float(np.sqrt(t.item())), float(np.sqrt(ss))
+
+
+# ---- the reference API on a multi-GPU job ---------------
+# inviscid_burgers_implicit2D / load_or_compute_snaps / run_fom.main under
+# torchrun: one process per GPU, every rank calls the reference function with
+# the reference's arguments (the WHOLE grid and w0); each marches its row slab
+# and writes its u rows and its v rows straight into ONE .npy file of the
+# whole (2 nx ny, ncols) matrix (burg_run_npy_ex, pwrite at the rows' byte
+# offsets), which every rank then maps.
+
+def job():
+    """(torch.distributed or None, rank, world) of this process.  Under
+    torchrun (WORLD_SIZE > 1 in the environment) the default process group is
+    initialised on first use if the caller has not done so -- gloo: the
+    library moves no snapshot or halo data through it, only barriers, the
+    ring-name and file-name broadcasts and the error agreement.  A single
+    process: (None, 0, 1)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return None, 0, 1
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        dist.init_process_group("gloo")
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def job_device(device=None):
+    """The GPU of this rank: `device` if given, else LOCAL_RANK under a
+    multi-process job (one process per GPU), else 0."""
+    if device is not None:
+        return int(device)
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return int(os.environ.get("LOCAL_RANK", "0"))
+    return 0
+
+
+_slab_ctxs = {}
+
+
+def job_context(nx, ny, device, dist, rank, world, **opts):
+    """This rank's cached slab context of an nx x ny grid (make_slab_context:
+    every rank must come here together the first time).  A context whose
+    launch failed is replaced (its halo rings hold stale colours)."""
+    key = (int(device), int(nx), int(ny), int(world), int(rank),
+           tuple(sorted((k, v) for k, v in opts.items())))
+    ctx = _slab_ctxs.get(key)
+    if ctx is None:
+        ctx = _slab_ctxs[key] = make_slab_context(nx, ny, rank, world, device=device, dist=dist,
+                                                  **opts)
+    return ctx
+
+
+def drop_job_context(ctx):
+    for k, v in list(_slab_ctxs.items()):
+        if v is ctx:
+            del _slab_ctxs[k]
+            v.close()
+
+
+def npy_header(m, ncols):
+    """The .npy header burg_run_npy writes (and np.save's format 1.0 layout:
+    magic, version, little-endian length, the dict padded with spaces to a
+    64-byte boundary, newline) of a C-order float64 (m, ncols) array."""
+    d = "{'descr': '<f8', 'fortran_order': False, 'shape': (%d, %d), }" % (m, ncols)
+    pad = (64 - (10 + len(d) + 1) % 64) % 64
+    d = d + " " * pad + "\n"
+    return b"\x93NUMPY\x01\x00" + len(d).to_bytes(2, "little") + d.encode("latin1")
+
+
+def create_npy(path, m, ncols):
+    """A (m, ncols) float64 .npy file of the right size, zero-filled (sparse),
+    with burg_run_npy's header: the file every rank of a job writes its rows
+    into (burg_run_npy_ex with NPY_EXISTING checks the header and size)."""
+    hdr = npy_header(m, ncols)
+    with open(path, "wb") as f:
+        f.write(hdr)
+        f.truncate(len(hdr) + 8 * m * ncols)
+
+
+def _agree(dist, err):
+    """Every rank learns whether any rank failed: (first error message or
+    None).  Collective."""
+    msgs = [None] * dist.get_world_size()
+    dist.all_gather_object(msgs, None if err is None else f"{type(err).__name__}: {err}")
+    bad = [(r, m) for r, m in enumerate(msgs) if m is not None]
+    return None if not bad else "; ".join(f"rank {r}: {m}" for r, m in bad)
+
+
+def slabs_to_npy(ctx, w0, num_steps, path, snap_every, dist, rank, world):
+    """Collective: every rank marches its slab of the trajectory from the
+    whole-grid initial state w0 and writes its rows into the .npy file `path`
+    of the whole (2 nx ny, num_steps // snap_every + 1) matrix, which rank 0
+    creates first.  Raises on every rank if any rank failed (the file is then
+    removed).  Returns this rank's stats."""
+    nx, ny = ctx.nx, ctx.ny_total
+    ncols = int(num_steps) // int(snap_every) + 1
+    err = None
+    if rank == 0:
+        try:
+            create_npy(path, 2 * nx * ny, ncols)
+        except OSError as e:
+            err = e
+    bad = _agree(dist, err)
+    if bad:
+        raise RuntimeError(f"snapshot file {path}: {bad}")
+    st = None
+    try:
+        st = ctx.run_to_npy(slab_state(w0, nx, ny, rank, world), num_steps, path,
+                            snap_every=snap_every, flags=NPY_GLOBAL | NPY_EXISTING)
+    except Exception as e:  # noqa: BLE001  (agreed on below, re-raised on every rank)
+        err = e
+    bad = _agree(dist, err)
+    if bad:
+        drop_job_context(ctx)
+        if rank == 0 and os.path.exists(path):
+            os.remove(path)
+        dist.barrier()
+        raise RuntimeError(f"multi-GPU trajectory failed: {bad}")
+    return st
+
+
+def shared_tmp_path(dist, rank, suffix=".npy"):
+    """A fresh path every rank of the job agrees on, in BURG_SNAP_DIR or the
+    temporary directory (the ranks of one node share it)."""
+    box = [None]
+    if rank == 0:
+        d = os.environ.get("BURG_SNAP_DIR") or tempfile.gettempdir()
+        box[0] = os.path.join(d, f"burg_snaps_{os.getpid():x}{secrets.token_hex(6)}{suffix}")
+    dist.broadcast_object_list(box, src=0)
+    return box[0]

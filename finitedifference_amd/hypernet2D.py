@@ -37,6 +37,7 @@ import numpy as np
 import scipy.sparse as sp
 from scipy.sparse.linalg import LinearOperator
 
+from .dist import job, job_context, job_device, shared_tmp_path, slabs_to_npy
 from .grid import fom_coefficients, make_2D_grid  # noqa: F401  (re-export)
 from .solver import DEFAULT_TOL, get_context
 from .ecsw import (compute_ECSW_training_matrix_2D_gp,  # noqa: F401  (re-export)
@@ -74,16 +75,16 @@ def get_ops(grid_x, grid_y):
 
 def _ctx_for(grid_x, grid_y, dt, mu, device=0, allow_nonsquare=False, **opts):
     nx, ny = np.asarray(grid_x).size - 1, np.asarray(grid_y).size - 1
-    ctx = get_context(nx, ny, device, **opts)
+    ctx = get_context(nx, ny, job_device(device), **opts)
     ctx.set_problem(grid_x, grid_y, dt, mu, allow_nonsquare)
     return ctx
 
 
 def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver="march",
-                                snap_every=1, device=0, engine="pipe", tile_w=64,
+                                snap_every=1, device=None, engine="pipe", tile_w=64,
                                 tol=DEFAULT_TOL, par_passes=0, verbose=1, allow_nonsquare=False,
                                 newton_max_its=100, newton_rtol=1e-12, return_stats=False,
-                                out=None):
+                                out=None, stream_w=0, tiles_target=0):
     """Implicit (trapezoidal-flux) time stepping of the 2D inviscid Burgers FOM
     (C/hypernet2D.py:72-131) on an MI355X.
 
@@ -103,11 +104,30 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     nothing.  out: an existing
     (2n, num_steps//snap_every + 1) C-contiguous float64 array (e.g. a .npy
     memmap) the snapshots are written into and returned.
-    """
+
+    Multi-GPU (launched under torchrun, one process per GPU, WORLD_SIZE > 1):
+    every rank calls this with the same arguments -- the whole grid and w0, as
+    the reference -- and gets the whole snapshot matrix back.  Rank k marches
+    its row slab on GPU `device` (default LOCAL_RANK) with the one-way halo
+    streamed from rank k-1 during the launch, and writes
+    its u rows and v rows straight into one shared .npy file of the whole
+    matrix (BURG_SNAP_DIR or the temporary directory; burg_run_npy_ex), which
+    every rank then maps copy-on-write (np.load(mmap_mode="c"): the values of
+    the single-GPU run, bit for bit, writable, one copy in host memory for
+    the whole node) before the file is unlinked.  The march solver only;
+    stream_w / tiles_target: the slabs' pipe tiling (default: planned)."""
+    d, rank, world = job()
+    if world > 1:
+        return _implicit2D_job(d, rank, world, grid_x, grid_y, w0, dt, num_steps, mu,
+                               solver=solver, snap_every=snap_every, device=device,
+                               engine=engine, verbose=verbose, allow_nonsquare=allow_nonsquare,
+                               return_stats=return_stats, out=out, stream_w=stream_w,
+                               tiles_target=tiles_target)
     if verbose:
         print("Running HDM for mu1={}".format(mu[0]))
     ctx = _ctx_for(grid_x, grid_y, dt, mu, device, allow_nonsquare, tile_w=tile_w,
-                   par_passes=par_passes, tol=tol, engine=engine)
+                   par_passes=par_passes, tol=tol, engine=engine, stream_w=stream_w,
+                   tiles_target=tiles_target)
     snaps, stats, its, rel = ctx.run(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps),
                                      solver, newton_max_its, newton_rtol, int(snap_every),
                                      out=out)
@@ -122,6 +142,50 @@ def inviscid_burgers_implicit2D(grid_x, grid_y, w0, dt, num_steps, mu, *, solver
     if return_stats:
         stats = dict(stats, step_iters=its, step_rel=rel)
         return snaps, stats
+    return snaps
+
+
+def _job_ctx(d, rank, world, grid_x, grid_y, dt, mu, device, engine, allow_nonsquare, stream_w,
+             tiles_target):
+    nx, ny = np.asarray(grid_x).size - 1, np.asarray(grid_y).size - 1
+    if engine != "pipe":
+        raise ValueError("multi-GPU slabs run on the pipe engine")
+    ctx = job_context(nx, ny, job_device(device), d, rank, world, engine="pipe",
+                      stream_w=int(stream_w), tiles_target=int(tiles_target))
+    ctx.set_problem(grid_x, grid_y, dt, mu, allow_nonsquare)
+    return ctx
+
+
+def _job_check(solver, out):
+    if solver != "march":
+        raise ValueError("multi-GPU slabs run the march solver (solver='march')")
+    if out is not None:
+        raise ValueError("out= is not supported on a multi-GPU job (every rank gets the "
+                         "whole matrix as a copy-on-write map)")
+
+
+def _implicit2D_job(d, rank, world, grid_x, grid_y, w0, dt, num_steps, mu, *, solver,
+                    snap_every, device, engine, verbose, allow_nonsquare, return_stats, out,
+                    stream_w, tiles_target):
+    """inviscid_burgers_implicit2D on a multi-GPU job (its docstring)."""
+    _job_check(solver, out)
+    if verbose and rank == 0:
+        print("Running HDM for mu1={}".format(mu[0]))
+    ctx = _job_ctx(d, rank, world, grid_x, grid_y, dt, mu, device, engine, allow_nonsquare,
+                   stream_w, tiles_target)
+    path = shared_tmp_path(d, rank)
+    st = slabs_to_npy(ctx, np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), path,
+                      int(snap_every), d, rank, world)
+    snaps = np.load(path, mmap_mode="c")
+    d.barrier()  # every rank holds its map: the name can go
+    if rank == 0:
+        os.remove(path)
+    if verbose and rank == 0:
+        print("\n".join(" ... Working on timestep {}".format(i) for i in range(int(num_steps))))
+    if return_stats:
+        its = np.ones(int(num_steps), dtype=np.int32)
+        return snaps, dict(st, step_iters=its, step_rel=np.zeros(int(num_steps)), rank=rank,
+                           world=world)
     return snaps
 
 
@@ -454,7 +518,20 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
 
     A cache file with fewer columns than asked for is returned as it is,
     truncated to what it holds (the reference's np.load(fn)[:, :num_steps+1]);
-    recompute_short=True recomputes it instead and overwrites the file."""
+    recompute_short=True recomputes it instead and overwrites the file.
+
+    Multi-GPU (torchrun, WORLD_SIZE > 1; inviscid_burgers_implicit2D): every
+    rank calls this with the same arguments.  Rank 0 decides hit or miss; on
+    a miss the ranks march their slabs and write their rows straight into the
+    cache file (under its .partial name, renamed by rank 0 once every rank has
+    written -- the same bytes as the single-GPU direct=True file); either way
+    every rank returns the cache file's matrix as a copy-on-write map
+    (np.load(mmap_mode="c"), or "r" with mmap=True), so the node holds one
+    copy.  The march solver only."""
+    d, rank, world = job()
+    if world > 1:
+        return _load_or_compute_job(d, rank, world, mu, grid_x, grid_y, w0, dt, num_steps,
+                                    snap_folder, mmap, recompute_short, solver_kw)
     if not os.path.exists(snap_folder):
         os.makedirs(snap_folder)
     every = int(solver_kw.get("snap_every", 1))
@@ -480,8 +557,13 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
         ctx = _ctx_for(grid_x, grid_y, dt, mu, device, solver_kw.get("allow_nonsquare", False),
                        engine=solver_kw.get("engine", "pipe"))
         tmp = snap_fn + ".partial.npy"
-        ctx.run_to_npy(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), tmp,
-                       snap_every=every)
+        try:
+            ctx.run_to_npy(np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), tmp,
+                           snap_every=every)
+        except Exception:
+            if os.path.exists(tmp):  # never leave a partial cache behind
+                os.remove(tmp)
+            raise
         os.replace(tmp, snap_fn)
         print("Elapsed time: {:3.3e}".format(time.time() - t0))
         return np.load(snap_fn, mmap_mode="r" if mmap else None)
@@ -497,6 +579,45 @@ def load_or_compute_snaps(mu, grid_x, grid_y, w0, dt, num_steps, snap_folder="pa
     snaps = None if mmap else np.array(mm)
     _commit_cache(tmp, snap_fn, mm)
     return np.load(snap_fn, mmap_mode="r") if mmap else snaps
+
+
+def _load_or_compute_job(d, rank, world, mu, grid_x, grid_y, w0, dt, num_steps, snap_folder,
+                         mmap, recompute_short, solver_kw):
+    """load_or_compute_snaps on a multi-GPU job (its docstring)."""
+    kw = dict(solver_kw)
+    every = int(kw.pop("snap_every", 1))
+    _job_check(kw.pop("solver", "march"), kw.pop("out", None))
+    ncols = int(num_steps) // every + 1
+    snap_fn = param_to_snap_fn(mu, snap_folder=snap_folder,
+                               suffix=".npy" if every == 1 else f"+every{every}.npy")
+    box = [None]
+    if rank == 0:
+        os.makedirs(snap_folder, exist_ok=True)
+        hit = False
+        if snap_fn in get_saved_params(snap_folder=snap_folder):
+            hit = np.load(snap_fn, mmap_mode="r").shape[1] >= ncols or not recompute_short
+        box[0] = hit
+    d.broadcast_object_list(box, src=0)
+    mode = "r" if mmap else "c"
+    if box[0]:
+        if rank == 0:
+            print(f"Loading saved snaps for mu1={mu[0]}, mu2={mu[1]}")
+        return np.load(snap_fn, mmap_mode=mode)[:, :ncols]
+    if rank == 0:
+        print(f"Computing new snaps for mu1={mu[0]}, mu2={mu[1]}")
+    t0 = time.time()
+    ctx = _job_ctx(d, rank, world, grid_x, grid_y, dt, mu, kw.pop("device", None),
+                   kw.pop("engine", "pipe"), kw.pop("allow_nonsquare", False),
+                   kw.pop("stream_w", 0), kw.pop("tiles_target", 0))
+    tmp = snap_fn + ".partial.npy"
+    slabs_to_npy(ctx, np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), tmp, every, d,
+                 rank, world)
+    d.barrier()
+    if rank == 0:
+        os.replace(tmp, snap_fn)
+        print("Elapsed time: {:3.3e}".format(time.time() - t0))
+    d.barrier()
+    return np.load(snap_fn, mmap_mode=mode)
 
 
 def load_or_compute_snaps_sweep(mus, grid_x, grid_y, w0, dt, num_steps,

@@ -14,6 +14,7 @@ from . import _lib
 from .grid import fom_coefficients
 
 DEFAULT_TOL = 2.0 ** -50  # 4 ulp relative inflow motion
+NPY_GLOBAL, NPY_EXISTING = 1, 2  # burg_run_npy_ex flags (include/burgers.h)
 
 
 class FOMContext:
@@ -179,14 +180,17 @@ class FOMContext:
             warnings.warn(self._L.burg_last_error().decode(), _lib.NotConvergedWarning)
         return snaps, st.as_dict(), its, rel
 
-    def run_to_npy(self, w0, num_steps, path, snap_every=1):
+    def run_to_npy(self, w0, num_steps, path, snap_every=1, flags=0):
         """One trajectory written straight into the .npy file `path`
-        (burg_run_npy: pinned buffers, pwrite writer thread); returns stats
-        (loop_ms launch, flush_ms gathers + D2H, march_kernel_ms whole call)."""
+        (burg_run_npy_ex: pinned buffers, pwrite writer thread); returns stats
+        (loop_ms launch, flush_ms gathers + D2H, march_kernel_ms whole call).
+        flags: NPY_GLOBAL -- a slab context writes its rows at their places in
+        the whole grid's matrix; NPY_EXISTING -- into a file another rank made
+        (write_npy_header) instead of creating it (include/burgers.h)."""
         w0 = self._vec(w0, "w0")
         st = _lib.BurgStats()
-        _lib.check(self._L.burg_run_npy(self._h, _lib.dptr(w0), int(num_steps), int(snap_every),
-                                        str(path).encode(), ctypes.byref(st)))
+        _lib.check(self._L.burg_run_npy_ex(self._h, _lib.dptr(w0), int(num_steps), int(snap_every),
+                                           str(path).encode(), int(flags), ctypes.byref(st)))
         return st.as_dict()
 
     def upload(self, w):

@@ -54,7 +54,7 @@
 extern "C" {
 #endif
 
-#define BURG_ABI_VERSION 14
+#define BURG_ABI_VERSION 15
 
 enum burg_status {
     BURG_OK = 0,
@@ -109,6 +109,24 @@ typedef struct burg_stats {
                                     (the call then returns BURG_ENAN) */
     int64_t paired_launches;    /* pipe engine: launches that ran the paired-halves W = 16
                                    kernel (two cells per lane and diagonal) */
+    /* pipe engine, the LAST launch of the call (what a
+     * multi-GPU bench line reports per rank): */
+    double ramp_ms;             /* first workgroup entry -> the last compute wave's first
+                                   block (the pipeline fill, incl. waiting for the rank below) */
+    double halo_wait_ms;        /* first workgroup entry -> the first block of the strip fed by
+                                   the inbound halo ring (-1: no inbound halo) */
+    /* pipe engine, all launches of the call: blocks that waited for south
+     * inflow and their summed waiting time (wave-ms), by where the inflow
+     * comes from -- a strip of this GPU, or the inbound halo ring */
+    int64_t south_waits_local;
+    int64_t south_waits_halo;
+    double south_wait_ms_local;
+    double south_wait_ms_halo;
+    /* the context's bounds guards (the flat-pointer ring / transpose kernels,
+     * DESIGN.md section 6.1), over its lifetime: copy calls that checked the
+     * guard, and how many found it set (each of those returned BURG_EHIP) */
+    int64_t bounds_checks;
+    int64_t bounds_hits;
 } burg_stats;
 
 enum burg_engine {
@@ -131,6 +149,12 @@ const char *burg_last_error(void);
  * ._lib.source_id() computes the same digest from a checkout, so a test run
  * can show that the shipped binary was built from the tree it runs in. */
 const char *burg_build_id(void);
+/* The compile flags of this build's objects that change what the kernels do
+ * (HIPFLAGS and every -D knob of the Makefile's object rules), fixed at
+ * compile time: an A/B or race-screen build (e.g. -DBURG_COMM_PRIO=2) reports
+ * the same source id as the shipped one but different flags, so a test run
+ * can show that it loaded the default build ("default" + the flags). */
+const char *burg_build_flags(void);
 
 /* Host-only audit of the pipe engine's trajectory ring (no GPU, no context):
  * replays, for tile width W, a num_steps trajectory keeping every
@@ -347,6 +371,25 @@ int burg_sweep_device(burg_ctx *ctx, int nmu, const double *src_b, const double 
  * Single-trajectory rings only (BURG_ENOMEM when it does not fit in HBM). */
 int burg_run_npy(burg_ctx *ctx, const double *w0, int num_steps, int snap_every, const char *path,
                  burg_stats *stats);
+
+/* burg_run_npy with flags -- the multi-GPU form of load_or_compute_snaps'
+ * cache write (C/hypernet2D.py:3141-3143, BurgersFD_CleanFine/run_fom.py:28
+ * at 750^2 over 8 GPUs):
+ *   BURG_NPY_GLOBAL: the file holds the WHOLE grid's (2 nx ny_total, ncols)
+ *     matrix and this slab context writes its u rows at global rows
+ *     [row0 nx, (row0 + nrows) nx) and its v rows at nx ny_total + the same
+ *     (without BURG_NPY_EXISTING the file is created with that header and
+ *     size);
+ *   BURG_NPY_EXISTING: the file already exists with exactly that .npy header
+ *     and at least its size (made by one rank, e.g. rank 0, before a barrier;
+ *     BURG_EINVAL otherwise) -- it is neither truncated nor re-headed, so
+ *     every rank writes its rows into the one file during the same call.
+ * Every rank of a slab job calls this together (the march's halo streams
+ * between the ranks' launches).  flags = 0 is burg_run_npy. */
+#define BURG_NPY_GLOBAL 1
+#define BURG_NPY_EXISTING 2
+int burg_run_npy_ex(burg_ctx *ctx, const double *w0, int num_steps, int snap_every,
+                    const char *path, int flags, burg_stats *stats);
 
 /* ECSW hyper-reduction training matrix (compute_ECSW_training_matrix_2D,
  * C/hypernet2D.py:2719-2740), with the context's problem (grid, dt, mu of

@@ -37,6 +37,9 @@ def gpu():
     bid, sid = _lib.build_id(), _lib.source_id()
     assert bid == sid, (f"libburgers_hip.so build id {bid} != source id {sid} of this checkout: "
                         "rebuild (make -C finitedifference_amd/csrc)")
+    # a knob build (race screen, A/B) only when asked for explicitly (BURG_LIB)
+    assert _lib.is_default_build() or os.environ.get("BURG_LIB"), (
+        f"the loaded library is a knob build ({_lib.build_flags()}), not the default one")
     return _lib
 
 
@@ -50,7 +53,8 @@ def pytest_terminal_summary(terminalreporter):
         terminalreporter.write_line(f"libburgers_hip build id: unavailable ({e})")
         return
     terminalreporter.write_line(f"libburgers_hip build id {bid}, sources {sid}: "
-                                f"{'match' if bid == sid else 'MISMATCH'}")
+                                f"{'match' if bid == sid else 'MISMATCH'}; flags: "
+                                f"{_lib.build_flags()}")
 
 
 @pytest.fixture(autouse=True)

@@ -85,6 +85,12 @@ def main():
                 f.write(" ".join(repr(x) for x in (ss, g1, s1, g0, s0)))
     with open(os.path.join(out, f"slab{rank}.w"), "w") as f:
         f.write(str(st["stream_w"]))
+    import json
+    with open(os.path.join(out, f"slab{rank}.stats"), "w") as f:
+        json.dump({k: st[k] for k in ("ramp_ms", "halo_wait_ms", "south_waits_local",
+                                      "south_waits_halo", "south_wait_ms_local",
+                                      "south_wait_ms_halo", "bounds_checks", "bounds_hits",
+                                      "loop_ms")}, f)
     with open(os.path.join(out, f"slab{rank}.halo"), "w") as f:
         f.write("%d %d" % ctx.halo_modes())
     dist.barrier()

@@ -358,6 +358,19 @@ def test_slab_halo_two_processes_one_gpu(gpu, orc, tmp_path, N, world, T, halo):
     mode = 2 if halo == "device" else 1
     want = [(0 if r == 0 else mode, 0 if r == world - 1 else mode) for r in range(world)]
     assert _halo_modes(tmp_path, world) == want
+    # the launch diagnostics a multi-GPU bench line reports per rank (DESIGN.md
+    # section 7): rank 0 has no inbound halo; the others waited for it, within
+    # their launch's ramp; only a halo strip counts halo waits
+    import json
+    for r in range(world):
+        d = json.load(open(os.path.join(tmp_path, f"slab{r}.stats")))
+        assert 0 < d["ramp_ms"] < d["loop_ms"], (r, d)
+        if r == 0:
+            assert d["halo_wait_ms"] == -1 and d["south_waits_halo"] == 0, d
+        else:
+            assert 0 <= d["halo_wait_ms"] <= d["ramp_ms"], (r, d)
+        assert d["south_wait_ms_halo"] >= 0 and d["south_wait_ms_local"] >= 0
+        assert d["bounds_hits"] == 0 and d["bounds_checks"] >= 1
     from finitedifference_amd.dist import assemble_snaps
     parts = [np.load(os.path.join(tmp_path, f"slab{r}.npy")) for r in range(world)]
     snaps = assemble_snaps(parts, N, N)
@@ -1179,3 +1192,38 @@ def test_direct_npy_writer(gpu, tmp_path, monkeypatch):
         monkeypatch.setenv("BURG_NPY_WRITERS", nw)
         ctx.run_to_npy(w0, T, str(tmp_path / f"w{nw}.npy"))
         assert open(tmp_path / f"w{nw}.npy", "rb").read() == open(tmp_path / "ref.npy", "rb").read(), nw
+
+
+def test_direct_npy_writer_failure_returns(gpu, tmp_path, monkeypatch):
+    """A failed row-block copy in burg_run_npy (forced with the test knob
+    BURG_TEST_FAIL_NPY_BLOCK on block 0, a middle block and the last) returns
+    BURG_EHIP instead of hanging in the writer drain (the taken
+    pinned buffer goes back to the pool); the context then writes a correct
+    file.  burg_run_npy_ex: a file made for another matrix is refused
+    (NPY_EXISTING), and a slab-less context with NPY_GLOBAL writes the same
+    bytes as burg_run_npy."""
+    from finitedifference_amd._lib import BurgersError, BURG_EHIP, BURG_EINVAL
+    from finitedifference_amd.dist import create_npy
+    from finitedifference_amd.solver import NPY_EXISTING, NPY_GLOBAL
+    N, T = 200, 5
+    ctx = make_ctx(N)
+    w0 = np.ones(2 * N * N)
+    ref = ctx.run(w0, T)[0]
+    monkeypatch.setenv("BURG_NPY_BLOCK_ROWS", "4001")  # 20 row blocks
+    for blk in ("0", "7", "19"):
+        monkeypatch.setenv("BURG_TEST_FAIL_NPY_BLOCK", blk)
+        with pytest.raises(BurgersError) as ei:
+            ctx.run_to_npy(w0, T, str(tmp_path / "f.npy"))
+        assert ei.value.code == BURG_EHIP and "row block copy failed" in str(ei.value)
+    monkeypatch.delenv("BURG_TEST_FAIL_NPY_BLOCK")
+    ctx.run_to_npy(w0, T, str(tmp_path / "ok.npy"))
+    assert np.array_equal(np.load(tmp_path / "ok.npy"), ref)
+    ctx.run_to_npy(w0, T, str(tmp_path / "g.npy"), flags=NPY_GLOBAL)
+    assert open(tmp_path / "g.npy", "rb").read() == open(tmp_path / "ok.npy", "rb").read()
+    create_npy(str(tmp_path / "e.npy"), 2 * N * N, T + 1)
+    ctx.run_to_npy(w0, T, str(tmp_path / "e.npy"), flags=NPY_GLOBAL | NPY_EXISTING)
+    assert open(tmp_path / "e.npy", "rb").read() == open(tmp_path / "ok.npy", "rb").read()
+    create_npy(str(tmp_path / "bad.npy"), 2 * N * N, T)  # one column short
+    with pytest.raises(BurgersError) as ei:
+        ctx.run_to_npy(w0, T, str(tmp_path / "bad.npy"), flags=NPY_GLOBAL | NPY_EXISTING)
+    assert ei.value.code == BURG_EINVAL
