@@ -31,7 +31,7 @@ EXPORTS = (
     "burg_sweep_device", "burg_pod_rsvd_device",
     "burg_kernel_bench", "burg_sweep", "burg_ecsw_matrix", "burg_ecsw_block_device", "burg_lspg",
     "burg_pod", "burg_pod_rsvd", "burg_run_npy", "burg_run_npy_ex", "burg_build_id",
-    "burg_build_flags", "burg_ring_audit",
+    "burg_build_flags", "burg_ring_audit", "burg_ring_audit_ex",
 )
 KERNELS = {"residual": 0, "jvp": 1}
 
@@ -121,6 +121,7 @@ def load(path=None):
             "burg_last_error": (ctypes.c_char_p, []),
             "burg_build_id": (ctypes.c_char_p, []),
             "burg_ring_audit": (ctypes.c_int, [ctypes.c_int] * 4 + [ctypes.POINTER(ctypes.c_int64)]),
+            "burg_ring_audit_ex": (ctypes.c_int, [ctypes.c_int] * 5 + [ctypes.POINTER(ctypes.c_int64)]),
             "burg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.POINTER(_VP)]),
             "burg_ctx_create_slab": (ctypes.c_int, [ctypes.c_int] * 7 + [ctypes.c_char_p,
@@ -242,10 +243,12 @@ def is_default_build():
     return build_flags().endswith("knobs: none")
 
 
-def ring_audit(W, num_steps, snap_every=1, ring_cap=0):
-    """burg_ring_audit as a dict (host-only; no GPU needed)."""
+def ring_audit(W, num_steps, snap_every=1, ring_cap=0, paired=False):
+    """burg_ring_audit_ex as a dict (host-only; no GPU needed); paired: the
+    paired-halves W = 16 kernel's walk."""
     rep = (ctypes.c_int64 * 9)()
-    check(load().burg_ring_audit(int(W), int(num_steps), int(snap_every), int(ring_cap), rep))
+    check(load().burg_ring_audit_ex(int(W), int(num_steps), int(snap_every), int(ring_cap),
+                                    1 if paired else 0, rep))
     keys = ("accesses", "max_entry", "entries_per_tile", "out_of_range", "walk_mismatch",
             "retained_overwritten", "early_overwrite", "retained_states", "snap_every")
     return dict(zip(keys, list(rep)))

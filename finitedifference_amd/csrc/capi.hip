@@ -3410,10 +3410,20 @@ const char *burg_build_flags(void) { return BURG_BUILD_FLAGS; }
 // lane l of diagonal s holds local time s - l.
 int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t *report)
 {
+    return burg_ring_audit_ex(W, num_steps, snap_every, ring_cap, 0, report);
+}
+
+int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int flags, int64_t *report)
+{
     if (!report) return fail(BURG_EINVAL, "null report");
     if (!pipe_width_supported(W)) return fail(BURG_EINVAL, "W=%d: not a pipe-engine width", W);
     if (num_steps < 1 || snap_every < 1 || ring_cap < 0)
         return fail(BURG_EINVAL, "num_steps, snap_every >= 1, ring_cap >= 0");
+    if (flags & ~BURG_AUDIT_PAIRED) return fail(BURG_EINVAL, "unknown flags %#x", flags);
+    const bool paired = (flags & BURG_AUDIT_PAIRED) != 0;
+    // (the paired-halves kernel: W = 16, plain rings -- pipe_args)
+    if (paired && (W != 16 || (snap_every >= 2 && snap_every * W >= W + 64)))
+        return fail(BURG_EINVAL, "the paired walk runs W = 16 on plain rings only");
     const int U = pipe_block_of(W);
     const int k = snap_every;
     TrajMap mp;
@@ -3468,8 +3478,63 @@ int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t 
     }
     for (int lane = 0; lane < kWave; ++lane)
         for (int cl = 0; cl < W; ++cl) write(pos((long long)cl + lane - W), (long long)cl + lane - W, lane);
+    // paired-halves kernel (pipe.hip PAIR): per lane, the A cell's entry eA
+    // (+1 per paired diagonal, +9 past column 7) and B's at eA - 8 (own wrap);
+    // steady blocks (full 8-diagonal blocks with no wrap of eA .. eA + 15 and
+    // eB >= 0) take their entries from the block base instead -- both forms
+    // are replayed and compared with each other and with ring_pos of the
+    // standard W = 16 layout (cell (q, c) of lane r at diagonal 16 q + c + r)
+    if (paired) {
+        const long long K8 = 8 * K;
+        const long long total2 = K8 + 8 + kWave - 1;  // lane 63's B cell ends at local time 8K + 7
+        const unsigned Lu = (unsigned)mp.L;
+        unsigned eA[kWave];
+        for (int lane = 0; lane < kWave; ++lane) {
+            long long e0l = mp.origin + 16LL * (((long long)-lane) >> 3) + ((-lane) & 7) + lane;
+            e0l %= mp.L;
+            eA[lane] = (unsigned)(e0l < 0 ? e0l + mp.L : e0l);
+        }
+        for (long long sb = 0; sb < total2; sb += 8) {
+            // the kernel's steady test (a full strip assumed), wave-uniform
+            bool steady = sb >= 72 && sb + 8 <= K8;
+            for (int lane = 0; lane < kWave && steady; ++lane)
+                steady = !(eA[lane] < 8u || eA[lane] + 15u >= Lu);
+            for (int lane = 0; lane < kWave; ++lane) {
+                const unsigned base = eA[lane];  // the block's first A entry
+                const int c0 = (int)((sb - lane) & 7);
+                const int uw8 = c0 == 0 ? 8 : ((8 - c0) & 7);  // A reaches column 0 (next step)
+                for (int u = 0; u < 8; ++u) {
+                    const long long tau = sb + u - lane;
+                    const long long cA = tau & 7, qA = tau >> 3;  // (floor division)
+                    const bool vA = tau >= 0 && tau < K8, vB = tau >= 8 && tau - 8 < K8;
+                    const unsigned wa = eA[lane];
+                    const unsigned wb = wa >= 8u ? wa - 8u : wa + Lu - 8u;
+                    // steady2: A at base + u (+ 8 from uw8 on), B 8 below
+                    if (steady) {
+                        const unsigned ra = base + (unsigned)u + (u < uw8 ? 0u : 8u);
+                        if (ra != wa || ra - 8u != wb) ++mism;
+                    }
+                    const long long dA = 16 * qA + cA + lane, dB = dA - 8;
+                    if (vA) {
+                        chk(wa, dA, true);
+                        write_entry(wa, dA);
+                        write(wa, dA, lane);
+                    }
+                    if (vB) {
+                        chk(wb, dB, true);
+                        write_entry(wb, dB);
+                        write(wb, dB, lane);
+                    }
+                    eA[lane] += cA == 7 ? 9u : 1u;
+                    if (eA[lane] >= Lu) eA[lane] -= Lu;
+                }
+                if (steady && eA[lane] != (base + 16u >= Lu ? base + 16u - Lu : base + 16u))
+                    ++mism;  // steady2: eA += 16 (wrapped once at Lu)
+            }
+        }
+    }
     // compute waves: one store per diagonal (lanes with local time in [0, KW))
-    {
+    if (!paired) {
         RetCursor rc;
         rc.init(ra, W, 0);
         unsigned pw = (unsigned)mp.origin;

@@ -169,6 +169,15 @@ const char *burg_build_flags(void);
  * before the loader read them, retained states, snap_every used.  Returns
  * BURG_OK when the plan exists (the counts say whether it is sound). */
 int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t *report);
+/* The same with flags: BURG_AUDIT_PAIRED replays the paired-halves W = 16
+ * kernel's store walk instead of the one-cell walk (two cells per lane and
+ * diagonal: the A cell's entry +1 per diagonal, +9 past column 7, the B cell
+ * 8 entries below with its own wrap, and the steady blocks' block-base
+ * entries, checked against the per-diagonal walk and ring_pos; plain rings,
+ * W = 16). */
+#define BURG_AUDIT_PAIRED 1
+int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int flags,
+                       int64_t *report);
 
 /* Create a context on HIP device `device` for an nx x ny grid (single GPU). */
 int burg_ctx_create(int device, int nx, int ny, burg_ctx **out);

@@ -53,6 +53,39 @@ def test_ring_indices_in_range_and_consistent(W, T, k, cap):
         assert r["retained_states"] == cap + 1
 
 
+# the paired-halves W = 16 kernel (pipe.hip PAIR): the default for
+# W = 16 sweeps and long trajectories -- the 1024^2 x 500 trajectory and the
+# 9-mu sweep's K = 4500 steps, short runs, and capped rings that wrap inside
+# the launch
+PAIRED = [(16, 500, 1, 0), (16, 4500, 1, 0), (16, 13, 1, 0), (16, 3, 1, 0), (16, 40, 1, 5),
+          (16, 120, 1, 7), (16, 2, 1, 0)]
+
+
+@pytest.mark.parametrize("W,T,k,cap", PAIRED)
+def test_paired_walk_in_range_and_consistent(W, T, k, cap):
+    r = _lib.ring_audit(W, T, k, cap, paired=True)
+    assert r["accesses"] >= 2 * 8 * T * 64, r  # two cells per lane and paired diagonal
+    assert r["out_of_range"] == 0, r
+    assert 0 <= r["max_entry"] < r["entries_per_tile"], r
+    assert r["walk_mismatch"] == 0, r  # per-diagonal walk = steady blocks = ring_pos
+    assert r["retained_overwritten"] == 0, r
+    assert r["early_overwrite"] == 0, r
+    # the paired kernel keeps the same states as the one-cell kernel
+    assert r["retained_states"] == _lib.ring_audit(W, T, k, cap)["retained_states"]
+
+
+def test_paired_audit_catches_a_wrong_walk():
+    """The paired replay is not vacuous: the one-cell walk's report differs
+    from the paired one (different accesses), and the paired mode refuses
+    widths and layouts the kernel never runs."""
+    a = _lib.ring_audit(16, 13, 1, 0)
+    b = _lib.ring_audit(16, 13, 1, 0, paired=True)
+    assert a["accesses"] != b["accesses"]
+    for bad in ((32, 13, 1, 0), (16, 13, 5, 0)):
+        with pytest.raises(_lib.BurgersError):
+            _lib.ring_audit(*bad, paired=True)
+
+
 def test_ring_audit_rejects_bad_arguments():
     with pytest.raises(_lib.BurgersError):
         _lib.ring_audit(48, 10, 1, 0)  # not a pipe width
