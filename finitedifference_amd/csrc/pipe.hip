@@ -110,6 +110,11 @@ constexpr unsigned G = kPipeGranuleStride;
 #ifndef BURG_LOADERS
 #define BURG_LOADERS 2
 #endif
+// BURG_AB_SKIP (A/B ceiling probe, wrong results): diagonals per W of the
+// wide tiles whose previous states the loader does not read back (0: off)
+#ifndef BURG_AB_SKIP
+#define BURG_AB_SKIP 0
+#endif
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
 #ifndef BURG_KLA
 #define BURG_KLA 16
@@ -160,8 +165,20 @@ constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
 // loader waves (BURG_LOADERS; at most 2 where two workgroups share a CU)
 template <int W>
 constexpr int nl_of() { return two_per_cu<W>() ? (BURG_LOADERS < 2 ? BURG_LOADERS : 2) : BURG_LOADERS; }
+// BURG_STORE_WAVE (A/B): the one-cell W = 16 kernels'
+// trajectory-ring stores issued by a sixth wave that copies each compute
+// wave's finished diagonals from its LDS state slots, so the compute waves
+// hold no ring-store VGPRs across diagonals (0: the compute waves store)
+#ifndef BURG_STORE_WAVE
+#define BURG_STORE_WAVE 0
+#endif
 template <int W>
-constexpr int threads_of() { return W > 16 ? (5 + nl_of<W>()) * kWave : 5 * kWave; }  // + loader wave(s)
+constexpr bool store_wave_of() { return BURG_STORE_WAVE && W == 16; }
+template <int W>
+constexpr int threads_of()
+{
+    return W > 16 ? (5 + nl_of<W>()) * kWave : (store_wave_of<W>() ? 6 : 5) * kWave;  // + loader / store wave
+}
 // Blocks of 16 diagonals for W = 128 ... 1024 (round 3 for 128, 256; window
 // 32 diagonals, LDS rings of 2 steps between the workgroup's waves -- the
 // room for it; the LDS DMA reaches past 64 KB, tools/probes/
@@ -779,6 +796,18 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 if ((k * nl_of<W>()) >> 2 != lw) continue;  // (this loader's compute waves)
                 const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
                 const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
+#if BURG_AB_SKIP > 0
+                // A/B ceiling probe only (WRONG results):
+                // the blocks of diagonals 64 .. 64 + BURG_AB_SKIP of every W
+                // (after the first W) are not read back from the ring -- the
+                // rate a read-back cut of that share could reach at most
+                if (nf[k] < lim && nf[k] >= W && (unsigned)((nf[k] & (W - 1)) - 64) < (unsigned)BURG_AB_SKIP) {
+                    nf[k] += U;
+                    if (lane == 0) lds_sti(&sm.filled[k], nf[k]);  // (earlier blocks: published)
+                    left |= nf[k] < total;
+                    continue;
+                }
+#endif
                 if (nf[k] < lim) {
                     const __amdgpu_buffer_rsrc_t ring =
                         rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
@@ -878,6 +907,84 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             }
         }
         return;
+    }
+    if constexpr (!WIDE && store_wave_of<W>()) {
+        if (wave == 5) {
+            // ================= store wave (BURG_STORE_WAVE) =================
+            // copies diagonal d of compute wave k from its LDS state slot
+            // d mod W to the tile's ring entry -- the walk of the compute
+            // wave's own stores (pw from origin with a wrap at L, or the
+            // retained-window cursor per block) -- once the wave has moved
+            // past d's block (prog), and publishes done[k] (diagonals
+            // copied), which the compute wave's readiness test waits for
+            // before it overwrites a slot (W diagonals later)
+            if constexpr (PAIR) return;  // (the paired kernel stores itself)
+            const int totalb = (KW + kWave - 1 + U - 1) / U * U;
+            const unsigned Lu = (unsigned)a.L;
+            int cp[4] = {0, 0, 0, 0};
+            unsigned pw4[4];
+            RetCursor rc4[4];
+            const bool ret = a.ret_k > 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                pw4[k] = (unsigned)a.origin;
+                rc4[k].init(a, W, 0);
+            }
+            v4u kv[U];  // the previous block's store data and offsets, kept live (store VGPRs)
+            unsigned ko[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                kv[u] = v4u{0u, 0u, 0u, 0u};
+                ko[u] = 0u;
+            }
+            static_assert(U == 8, "store wave: blocks of 8");
+            long long t_prog = now_rt();
+            for (;;) {
+                bool left = false, any = false;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (k >= nval) continue;
+                    if (cp[k] < totalb && cp[k] + U <= lds_ldi(&sm.prog[k])) {
+                        const __amdgpu_buffer_rsrc_t ring =
+                            rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
+                        unsigned e = ret ? rc4[k].next(a, W, U) : pw4[k];
+                        v4u v[U];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) v[u] = lds_ld(&sm.st[k][(cp[k] + u) & (W - 1)][lane]);
+                        asm volatile("" ::"v"(kv[0]), "v"(kv[1]), "v"(kv[2]), "v"(kv[3]), "v"(kv[4]), "v"(kv[5]),
+                                     "v"(kv[6]), "v"(kv[7]));
+                        asm volatile("" ::"v"(ko[0]), "v"(ko[1]), "v"(ko[2]), "v"(ko[3]), "v"(ko[4]), "v"(ko[5]),
+                                     "v"(ko[6]), "v"(ko[7]));
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const int t = cp[k] + u - lane;
+                            unsigned o = (unsigned)t < (unsigned)KW ? e * 1024u + lane * 16u : kOOB;
+                            launder(o);
+                            st_plain(ring, o, v[u]);
+                            kv[u] = v[u];
+                            ko[u] = o;
+                            e = (!ret && e + 1 == Lu) ? 0u : e + 1;
+                        }
+                        if (!ret) pw4[k] = e;
+                        cp[k] += U;
+                        // (the slots' reads have returned -- the stores used
+                        // them -- so the compute wave may overwrite them)
+                        if (lane == 0) lds_sti(&sm.done[k], cp[k]);
+                        any = true;
+                    }
+                    left |= cp[k] < totalb;
+                }
+                if (!left || lds_ldi(&sm.perm[5])) break;
+                const long long tn = now_rt();
+                if (any) {
+                    t_prog = tn;
+                } else {
+                    if (tn - t_prog > a.spin_ticks) break;  // (the compute waves time out themselves)
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            return;
+        }
     }
     if (wave >= nval) return;
 
@@ -1543,6 +1650,10 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         if constexpr (WIDE) {
             if (any_lane(lds_ldi(&sm.filled[k]) < sb + U)) why |= 32u;
         }
+        // store wave: the block's slots (diagonals sb - W .. sb - W + U) copied
+        if constexpr (!WIDE && store_wave_of<W>()) {
+            if (lds_ldi(&sm.done[k]) < sb - W + U) why |= 64u;
+        }
         return why;
     };
 
@@ -1574,6 +1685,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         const bool miss_n = has_north & (th >= 0) & (th >= pn);
         bool miss = miss_w | miss_s | miss_e | miss_n;
         if constexpr (WIDE) miss = miss | (lds_ldi(&sm.filled[k]) < sb + U);
+        if constexpr (!WIDE && store_wave_of<W>()) miss = miss | (lds_ldi(&sm.done[k]) < sb - W + U);
         return __builtin_amdgcn_ballot_w64(miss) == 0;
     };
 
@@ -1678,7 +1790,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         unsigned ro;        // the ring store's voffset
         unsigned eoff = kOOB, noff = kOOB;  // the east / north stores' voffsets
         v4u outk = out;
-        if constexpr (STEADY) {
+        if constexpr (!WIDE && store_wave_of<W>()) {
+            ro = 0u;  // (the store wave copies the LDS state slots to the ring)
+        } else if constexpr (STEADY) {
             ro = lane16;
             launder(ro);
             if constexpr (WIDE) __builtin_amdgcn_raw_buffer_store_b128(outk, ring, ro, pw * 1024u, BURG_RING_AUX);
@@ -1969,6 +2083,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // end exactly at the ring's end: the next store goes to entry 0)
         if (steady && pw == Lu) pw = 0u;
     }
+    // store wave: the last block is finished too
+    if constexpr (!WIDE && store_wave_of<W>()) lds_sti(lane == 0 ? &sm.prog[k] : sink_i, total + U);
     if (lane == 0) {
         if (spins) atomicAdd(&a.stats->stall_spins, spins);
         if (slow_n) atomicAdd(&a.stats->slow_diagonals, slow_n);

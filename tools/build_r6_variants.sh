@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-6 knob builds (rebuild after every source change: the GPU tests
+# refuse a library whose build id differs from the sources)
+set -e
+cd "$(dirname "$0")/.."
+make -s -j8 -C finitedifference_amd/csrc
+tools/probes/build_variant.sh cp2 "-DBURG_COMM_PRIO=2"
+for n in 32 64 128; do tools/probes/build_variant.sh skip$n "-DBURG_AB_SKIP=$n"; done
+tools/probes/build_variant.sh sw "-DBURG_STORE_WAVE=1"
