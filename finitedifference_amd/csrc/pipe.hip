@@ -356,19 +356,26 @@ __device__ __forceinline__ bool any_lane(bool b) { return __builtin_amdgcn_ballo
 
 // (RetCursor, the retained-window walk: burg_internal.h)
 
-// Launch diagnostics of one compute wave (lane 0, once, at its end;
-// DESIGN.md section 7): when its first block could start (the latest over
-// the launch = the ramp; the earliest over the slab's halo strip = the wait
-// for the rank below), and its blocks that waited for south inflow, split by
-// where that inflow comes from (the halo ring / a strip of this GPU).
-__device__ __forceinline__ void launch_diag(const PipeArgs &a, bool halo, long long first,
-                                            unsigned south_blocks, unsigned long long south_rt)
+// Launch diagnostics of one compute wave, recorded
+// outside the hot path and with no loop-carried registers: when its first
+// block could start (lane 0, once; the latest over the launch = the ramp,
+// the earliest over the slab's halo strip = the wait for the rank below),
+// the time each of its blocks waited for south inflow (lane 0, in the wait
+// path), and at its end the number of such blocks -- split by where that
+// inflow comes from (the halo ring / a strip of this GPU).
+__device__ __forceinline__ void diag_first(const PipeArgs &a, bool halo)
 {
-    atomicMax(&a.stats->t_first_max, (unsigned long long)first);
-    if (halo) atomicMin(&a.stats->t_halo_first, (unsigned long long)first);
-    const int h = halo ? 1 : 0;
-    if (south_blocks) atomicAdd(&a.stats->south_blocks[h], (unsigned long long)south_blocks);
-    if (south_rt) atomicAdd(&a.stats->south_rt[h], south_rt);
+    const unsigned long long t = (unsigned long long)now_rt();
+    atomicMax(&a.stats->t_first_max, t);
+    if (halo) atomicMin(&a.stats->t_halo_first, t);
+}
+__device__ __forceinline__ void diag_south_wait(const PipeArgs &a, bool halo, long long t0)
+{
+    atomicAdd(&a.stats->south_rt[halo ? 1 : 0], (unsigned long long)(now_rt() - t0));
+}
+__device__ __forceinline__ void diag_south_blocks(const PipeArgs &a, bool halo, unsigned n)
+{
+    if (n) atomicAdd(&a.stats->south_blocks[halo ? 1 : 0], (unsigned long long)n);
 }
 
 
@@ -1398,10 +1405,6 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             if (eA >= Lu) eA -= Lu;
         };
         __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
-        // launch diagnostics: when the wave's first block could start, and
-        // the time its blocks waited for south inflow (s_memrealtime)
-        long long p_first = now_rt();
-        unsigned long long p_srt = 0;
         for (int sb = 0; sb < total2; sb += U) {
             lds_sti(lane == 0 ? &sm.prog[k] : sink, sb);
             if (__builtin_expect(missing2(sb, false) != 0, 0)) {
@@ -1436,12 +1439,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 }
                 if (waited) {
                     pwait += __builtin_amdgcn_s_memtime() - c0;
-                    const long long tw = now_rt();
-                    if (sb == 0) p_first = tw;
-                    if (wsouth) p_srt += (unsigned long long)(tw - t0);
+                    if (wsouth && lane == 0) diag_south_wait(a, south_host, t0);
                 }
                 if (paborted) break;
             }
+            if (sb == 0 && lane == 0) diag_first(a, south_host);
             bool steady = (a.pair == 1) & (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
                           !any_lane((eA < 8u) | (eA + 15u >= Lu));
             if constexpr (SWEEP)
@@ -1480,7 +1482,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             if (pwait) atomicAdd(&a.stats->slow_ticks, pwait);
             for (int i = 0; i < 5; ++i)
                 if (pwhy[i]) atomicAdd(&a.stats->why[i], (unsigned long long)pwhy[i]);
-            launch_diag(a, south_host, p_first, pwhy[3], p_srt);
+            diag_south_blocks(a, south_host, pwhy[3]);
             atomicAdd(&a.stats->tile_steps, (unsigned long long)K);
         }
         return;
@@ -1969,10 +1971,6 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     unsigned long long pf_vm = 0;
     const unsigned long long pf0 = __builtin_amdgcn_s_memtime();
 #endif
-    // launch diagnostics: when the wave's first block could start, and the
-    // time its blocks waited for south inflow (s_memrealtime)
-    long long d_first = now_rt();
-    unsigned long long d_srt = 0;
     for (int sb = 0; sb < total; sb += U) {
 #ifdef BURG_PIPE_PROF
         const unsigned long long pfa = __builtin_amdgcn_s_memtime();
@@ -2025,12 +2023,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             }
             if (waited) {
                 wait_ticks += __builtin_amdgcn_s_memtime() - c0;
-                const long long tw = now_rt();
-                if (sb == 0) d_first = tw;
-                if (wsouth) d_srt += (unsigned long long)(tw - t0);
+                if (wsouth && lane == 0) diag_south_wait(a, south_host, t0);
             }
             if (aborted) break;
         }
+        if (sb == 0 && lane == 0) diag_first(a, south_host);
         // (retained windows: the block's ring entries are consecutive and
         // never wrap; plain ring: wrap checked below)
         if (ret) pw = rcur.next(a, W, U);
@@ -2093,7 +2090,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         if (wait_ticks) atomicAdd(&a.stats->slow_ticks, wait_ticks);
         for (int i = 0; i < 5; ++i)
             if (wait_why[i]) atomicAdd(&a.stats->why[i], (unsigned long long)wait_why[i]);
-        launch_diag(a, south_host, d_first, wait_why[3], d_srt);
+        diag_south_blocks(a, south_host, wait_why[3]);
 #ifdef BURG_PIPE_PROF
         atomicAdd(&a.stats->prof[0], __builtin_amdgcn_s_memtime() - pf0);
         atomicAdd(&a.stats->prof[1], pf_vm);
