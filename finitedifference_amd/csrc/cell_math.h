@@ -147,7 +147,12 @@ struct MarchCell {
             // max and a compare.
             const unsigned xu = (unsigned)__double2hiint(cu) - (123u << 20);
             const unsigned xv = (unsigned)__double2hiint(cv) - (123u << 20);
+#ifdef BURG_AB_NOCHECK
+            range_ok = true;  // (A/B probes only: the fast path for every operand -- wrong in general)
+            (void)xu, (void)xv;
+#else
             range_ok = max(xu, xv) < (1698u << 20);
+#endif
             s = 0.5 + sqrt_normal(q);
             div2_normal(cu, cv, s, nu, nv);
         } else {

@@ -165,12 +165,14 @@ constexpr bool two_per_cu() { return BURG_TWO_PER_CU && (W == 64 || W == 128); }
 // loader waves (BURG_LOADERS; at most 2 where two workgroups share a CU)
 template <int W>
 constexpr int nl_of() { return two_per_cu<W>() ? (BURG_LOADERS < 2 ? BURG_LOADERS : 2) : BURG_LOADERS; }
-// BURG_STORE_WAVE (A/B): the one-cell W = 16 kernels'
-// trajectory-ring stores issued by a sixth wave that copies each compute
-// wave's finished diagonals from its LDS state slots, so the compute waves
-// hold no ring-store VGPRs across diagonals (0: the compute waves store)
+// BURG_STORE_WAVE (round 6): the
+// one-cell W = 16 kernels' trajectory-ring stores are issued by a sixth wave
+// that copies each compute wave's finished diagonals from its LDS state
+// slots, so the compute waves neither issue them nor hold their VGPRs across
+// diagonals: one 1024^2 trajectory -2.1 %, the one-cell 9-mu sweep -3.0 %
+// (profiles/r06/ab/store_wave).  0: the compute waves store (rounds 1-5).
 #ifndef BURG_STORE_WAVE
-#define BURG_STORE_WAVE 0
+#define BURG_STORE_WAVE 1
 #endif
 template <int W>
 constexpr bool store_wave_of() { return BURG_STORE_WAVE && W == 16; }
@@ -926,6 +928,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             // copied), which the compute wave's readiness test waits for
             // before it overwrites a slot (W diagonals later)
             if constexpr (PAIR) return;  // (the paired kernel stores itself)
+            // (BURG_STOREWAVE_PRIO: race-screen builds only)
+#ifndef BURG_STOREWAVE_PRIO
+#define BURG_STOREWAVE_PRIO 0
+#endif
+            __builtin_amdgcn_s_setprio(BURG_STOREWAVE_PRIO);
             const int totalb = (KW + kWave - 1 + U - 1) / U * U;
             const unsigned Lu = (unsigned)a.L;
             int cp[4] = {0, 0, 0, 0};

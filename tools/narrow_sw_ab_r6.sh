@@ -7,10 +7,10 @@
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-ab_sw}; mkdir -p $O
-BURG_LIB=finitedifference_amd/libburgers_hip_sw.so timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "pipe_1024 or pipe_bitwise_sequential or sweep_each or retained or slab_halo_two or sweep_1024 or run_fom_main or direct_npy" > $O/pytest_sw.log 2>&1 || { tail -30 $O/pytest_sw.log; exit 1; }
+BURG_LIB=$PWD/finitedifference_amd/libburgers_hip_sw.so timeout -k 10 600 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -k "pipe_1024 or pipe_bitwise_sequential or sweep_each or retained or slab_halo_two or sweep_1024 or run_fom_main or direct_npy" > $O/pytest_sw.log 2>&1 || { tail -30 $O/pytest_sw.log; exit 1; }
 tail -1 $O/pytest_sw.log
 for r in 1 2 3; do for v in base sw; do
-  L=finitedifference_amd/libburgers_hip.so; [ $v = sw ] && L=finitedifference_amd/libburgers_hip_sw.so
+  L=$PWD/finitedifference_amd/libburgers_hip.so; [ $v = sw ] && L=$PWD/finitedifference_amd/libburgers_hip_sw.so
   BURG_LIB=$L timeout -k 10 300 python3 -c "
 import json, bench
 s = bench.single_1024(bench.os.path.join(bench.ROOT, 'profiles', 'pmc_traffic.json'), bench.os.path.join(bench.ROOT, 'profiles', 'r05', 'pipe_isa.json'))
