@@ -115,6 +115,18 @@ constexpr unsigned G = kPipeGranuleStride;
 #ifndef BURG_AB_SKIP
 #define BURG_AB_SKIP 0
 #endif
+// BURG_KEEP_BLOCK (round 6): the
+// wide tiles keep the outputs of ONE block of U diagonals per W -- the block
+// at diagonal kKeepS mod W -- in VGPRs of the compute wave, and read the next
+// step's previous states of that block from there instead of the HBM ring
+// (the loader skips their read-back); 0: every previous state from the ring
+#ifndef BURG_KEEP_BLOCK
+#define BURG_KEEP_BLOCK 0
+#endif
+constexpr int kKeepS = 64;  // (a steady / interior block for every W >= 128)
+template <int W>
+constexpr bool keep_of() { return BURG_KEEP_BLOCK && (W == 128 || W == 256); }  // (W >= 512: the loader's
+                                                                                 // column-table DMAs ride with the window's)
 constexpr int kSL = 16;   // comm lanes per compute wave for the south / north streams
 #ifndef BURG_KLA
 #define BURG_KLA 16
@@ -805,12 +817,24 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 if ((k * nl_of<W>()) >> 2 != lw) continue;  // (this loader's compute waves)
                 const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
                 const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
+                if constexpr (keep_of<W>()) {
+                    // the kept block's previous states are in the compute
+                    // wave's registers (after the first W diagonals): no read
+                    if (nf[k] < lim && nf[k] >= W && (nf[k] & (W - 1)) == kKeepS) {
+                        if (ret) (void)rc[k].next(a, W, U);  // (the walk moves on)
+                        nf[k] += U;
+                        if (lane == 0) lds_sti(&sm.filled[k], nf[k]);  // (earlier blocks: published)
+                        left |= nf[k] < total;
+                        continue;
+                    }
+                }
 #if BURG_AB_SKIP > 0
                 // A/B ceiling probe only (WRONG results):
                 // the blocks of diagonals 64 .. 64 + BURG_AB_SKIP of every W
                 // (after the first W) are not read back from the ring -- the
                 // rate a read-back cut of that share could reach at most
                 if (nf[k] < lim && nf[k] >= W && (unsigned)((nf[k] & (W - 1)) - 64) < (unsigned)BURG_AB_SKIP) {
+                    if (ret) (void)rc[k].next(a, W, U);
                     nf[k] += U;
                     if (lane == 0) lds_sti(&sm.filled[k], nf[k]);  // (earlier blocks: published)
                     left |= nf[k] < total;
@@ -1618,6 +1642,17 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         in.gs = lds_ld(b.ib + u);
         return in;
     };
+    // the same without the previous state (the kept block: keep_of)
+    auto fetch_b_nx = [&](const Bases &b, int u) -> In {
+        In in;
+        in.nt = false;
+        in.src = 0.0;
+        in.xs = v4u{0u, 0u, 0u, 0u};
+        in.cs = cc_ld(b.cb + u);
+        in.gw = v4u{0u, 0u, 0u, 0u};
+        in.gs = lds_ld(b.ib + u);
+        return in;
+    };
 
     // Readiness of a whole block of diagonals [sb, sb + U): every inflow it
     // consumes is deposited, every outbound slot it fills is granted and (wide
@@ -1699,7 +1734,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     };
 
     // one diagonal, diagonal u of its block (no waits: the block was checked)
-    auto diagonal = [&](auto edge_tag, const int s, const int u, In &in) {
+    auto diagonal = [&](auto edge_tag, const int s, const int u, In &in) -> v4u {
         constexpr bool EDGE = decltype(edge_tag)::value == 0;
         constexpr bool SE = decltype(edge_tag)::value >= 3;
         // (narrow steady-edge blocks come in two builds: 4 for the
@@ -1898,6 +1933,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             }
         }
         (void)u;
+        return out;
     };
 
     // One block: the LDS inputs are read two diagonals ahead (their latency
@@ -1905,7 +1941,15 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     // was checked ready by block_missing.  Sweeps read one ahead, after the
     // diagonal: a lane's trajectory switch (in diagonal s) decides which
     // state and source table diagonal s + 1 reads.
-    auto run_block = [&](auto tag, const int sb) {
+    // the kept block's outputs (keep_of: VGPRs, one block per W)
+    v4u kr[keep_of<W>() ? uw_of<W>() : 1];
+#pragma unroll
+    for (int u = 0; u < (keep_of<W>() ? uw_of<W>() : 1); ++u) kr[u] = v4u{0u, 0u, 0u, 0u};
+    auto run_block = [&](auto tag, const int sb, auto keep_tag) {
+        // KEEP: the kept block -- previous states from kr once the first W
+        // diagonals are past (before that the loader read them), outputs to kr
+        constexpr bool KEEP = decltype(keep_tag)::value;
+        const bool reg_ok = KEEP && sb >= W;
         if constexpr (SWEEP && decltype(tag)::value < 3) {
             In a0 = fetch(tag, sb);
 #pragma unroll
@@ -1946,12 +1990,31 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 se_eoff = (east_glob & oute) ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             }
             const Bases b = bases_of(sb);
-            In a0 = fetch_b(b, 0), a1 = fetch_b(b, 1);
+            if constexpr (KEEP) {
+                // the first W diagonals: the kept block's previous states came
+                // through the loader's window (once per launch)
+                if (!reg_ok) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) kr[u] = lds_ld(b.wb + u * kWave);
+                }
+            }
+            // (KEEP: the previous state is kr[u], not loaded into In)
+            auto fb = [&](int u) -> In {
+                if constexpr (KEEP) {
+                    In in = fetch_b_nx(b, u);
+                    in.xs = kr[u];
+                    return in;
+                } else {
+                    return fetch_b(b, u);
+                }
+            };
+            In a0 = fb(0), a1 = fb(1);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 In nx;
-                if (u + 2 < U) nx = fetch_b(b, u + 2);
-                diagonal(tag, sb + u, u, a0);
+                if (u + 2 < U) nx = fb(u + 2);
+                const v4u o = diagonal(tag, sb + u, u, a0);
+                if constexpr (KEEP) kr[u] = o;
                 a0 = a1;
                 if (u + 2 < U) a1 = nx;
             }
@@ -2073,15 +2136,25 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             if ((W == 16 || W > kWave) && steady) {
                 // (narrow tiles only: the wide kernel measured 0.6 % slower
                 // with the two builds, profiles/r03/ab/steady_edge_east.txt)
-                if (!WIDE && east_glob) run_block(SteadyEdgeG(), sb);
-                else run_block(SteadyEdge(), sb);
+                if (!WIDE && east_glob) run_block(SteadyEdgeG(), sb, std::false_type());
+                else run_block(SteadyEdge(), sb, std::false_type());
             } else {
-                run_block(Edge(), sb);
+                run_block(Edge(), sb, std::false_type());
             }
         } else if (steady) {
-            run_block(Steady(), sb);
+            if constexpr (keep_of<W>()) {
+                if (sm_ == kKeepS) run_block(Steady(), sb, std::true_type());
+                else run_block(Steady(), sb, std::false_type());
+            } else {
+                run_block(Steady(), sb, std::false_type());
+            }
         } else {
-            run_block(Interior(), sb);
+            if constexpr (keep_of<W>()) {
+                if (sm_ == kKeepS) run_block(Interior(), sb, std::true_type());
+                else run_block(Interior(), sb, std::false_type());
+            } else {
+                run_block(Interior(), sb, std::false_type());
+            }
         }
         // a steady block advances the ring pointer without wrapping (it may
         // end exactly at the ring's end: the next store goes to entry 0)
