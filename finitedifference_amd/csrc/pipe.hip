@@ -94,11 +94,18 @@ constexpr unsigned kLdsEmptyHi = 0x7FF6DEADu;  // LDS slot empty
 constexpr unsigned kOOB = 0xC0000000u;  // past every buffer's range: loads 0, stores dropped
 constexpr int kR = kPipeR;
 constexpr unsigned G = kPipeGranuleStride;
-// BURG_DMA_READBACK: the loader reads each block's LDS-DMA bytes back before
-// it publishes filled[] (see the loader wave).  0 = rounds 2-4's protocol
-// (publish right after the covering vmcnt).
+// BURG_DMA_READBACK: 1 = the loader reads each block's LDS-DMA bytes back
+// before it publishes filled[] (round 5, defensive); 0 = publish right after
+// the covering vmcnt (rounds 2-4, and the default again in round 6).  The
+// covering vmcnt is what orders the DMA'd bytes for the issuing wave, and the
+// filled[] flag, written after it and polled by the compute wave before its
+// reads, plays the barrier's part for the other waves (MI355X_MICROARCH.md
+// item 7); round 5's wrong window rows were the store-VGPR hazard (DESIGN.md
+// section 6.2), not the DMA.  Without the read-back: 4096^2 +1.3 % (3
+// interleaved rounds, profiles/r06/ab/aux/), the wide bitwise tests and the
+// race screens with the loader / comm wave above the compute waves green.
 #ifndef BURG_DMA_READBACK
-#define BURG_DMA_READBACK 1
+#define BURG_DMA_READBACK 0
 #endif
 // BURG_LOADERS: loader waves per wide workgroup.  2 (round 5) = wave 5 fills
 // compute waves 0-1's windows, wave 6 those of waves 2-3: twice the ring DMAs
