@@ -131,6 +131,12 @@ constexpr unsigned G = kPipeGranuleStride;
 #define BURG_KEEP_BLOCK 0
 #endif
 constexpr int kKeepS = 64;  // (a steady / interior block for every W >= 128)
+// BURG_KEEP_BLOCK=2: only the block's first half (8 diagonals, 32 VGPRs) is
+// kept; the loader reads its other half back as usual
+template <int W>
+constexpr int uw_of();
+template <int W>
+constexpr int keep_n_of() { return BURG_KEEP_BLOCK == 2 ? uw_of<W>() / 2 : uw_of<W>(); }
 template <int W>
 constexpr bool keep_of() { return BURG_KEEP_BLOCK && (W == 128 || W == 256); }  // (W >= 512: the loader's
                                                                                  // column-table DMAs ride with the window's)
@@ -818,13 +824,17 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         for (;;) {
             bool left = false;
             int got[4] = {0, 0, 0, 0};  // blocks issued this round, per wave
+            int nld[4] = {0, 0, 0, 0};  // their loads
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (k >= nval) continue;
                 if ((k * nl_of<W>()) >> 2 != lw) continue;  // (this loader's compute waves)
                 const int pk = lds_ldi(&sm.prog[k]), dk = lds_ldi(&sm.done[k]);
                 const int lim = min(min(total, pk + KWIN), dk + W);  // multiples of U
-                if constexpr (keep_of<W>()) {
+                // (kept half block: only its last U - KN rows are read back)
+                const bool khalf = keep_of<W>() && keep_n_of<W>() < U && nf[k] >= W &&
+                                   (nf[k] & (W - 1)) == kKeepS;
+                if constexpr (keep_of<W>() && keep_n_of<W>() == U) {
                     // the kept block's previous states are in the compute
                     // wave's registers (after the first W diagonals): no read
                     if (nf[k] < lim && nf[k] >= W && (nf[k] & (W - 1)) == kKeepS) {
@@ -859,6 +869,13 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                         e = e < 0 ? e + L : e;
                     }
                     int slot = nf[k] % KWIN;
+                    if (khalf) {
+                        // (a block's U entries are consecutive: plain ring
+                        // with a wrap, retained windows without one)
+                        constexpr int KN = keep_n_of<W>() < U ? keep_n_of<W>() : 0;
+                        e = ret ? e + KN : (e + KN >= L ? e + KN - L : e + KN);  // (windows lie past L)
+                        slot += KN;
+                    }
                     if constexpr (ccw_of<W>()) {
                         // the block's U columns into the rolling table (slot
                         // t mod kCCW, and its padding copy for the first U
@@ -874,12 +891,25 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                                                                      co, 0, 0, 0);
                         }
                     }
+                    if (khalf) {
+                        constexpr int KN = keep_n_of<W>() < U ? keep_n_of<W>() : 0;
 #pragma unroll
-                    for (int u = 0; u < U; ++u) {
-                        __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
-                                                                 (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
-                        e = e + 1 == L ? 0 : e + 1;
-                        slot = slot + 1 == KWIN ? 0 : slot + 1;
+                        for (int u = KN; u < U; ++u) {
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
+                                                                     (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
+                            e = e + 1 == L ? 0 : e + 1;
+                            slot = slot + 1 == KWIN ? 0 : slot + 1;
+                        }
+                        nld[k] = U - KN;
+                    } else {
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(ring, (LDS void *)&sm.win[k][slot][0], 16,
+                                                                     (unsigned)e * 1024u + lane * 16u, 0, 0, BURG_LOAD_AUX);
+                            e = e + 1 == L ? 0 : e + 1;
+                            slot = slot + 1 == KWIN ? 0 : slot + 1;
+                        }
+                        nld[k] = U + (ccw_of<W>() ? 2 : 0);
                     }
                     nf[k] += U;
                     got[k] = 1;
@@ -892,15 +922,32 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 // after it) loads are outstanding
                 constexpr int NB = U + (ccw_of<W>() ? 2 : 0);  // loads per block
                 int after = nb;
+                // (kept half blocks: the loads issued after wave k's, counted
+                // exactly -- multiples of 8 up to 3 x 16)
+                int la = nld[0] + nld[1] + nld[2] + nld[3];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     if (!got[k]) continue;
                     --after;
-                    switch (after) {
-                    case 0: wait_vmcnt<0>(); break;
-                    case 1: wait_vmcnt<NB>(); break;
-                    case 2: wait_vmcnt<2 * NB>(); break;
-                    default: wait_vmcnt<3 * NB>(); break;
+                    la -= nld[k];
+                    if constexpr (keep_of<W>() && keep_n_of<W>() < U) {
+                        static_assert(NB == 16 && U == 16, "kept half blocks: blocks of 16 rows");
+                        switch (la >> 3) {
+                        case 0: wait_vmcnt<0>(); break;
+                        case 1: wait_vmcnt<8>(); break;
+                        case 2: wait_vmcnt<16>(); break;
+                        case 3: wait_vmcnt<24>(); break;
+                        case 4: wait_vmcnt<32>(); break;
+                        case 5: wait_vmcnt<40>(); break;
+                        default: wait_vmcnt<48>(); break;
+                        }
+                    } else {
+                        switch (after) {
+                        case 0: wait_vmcnt<0>(); break;
+                        case 1: wait_vmcnt<NB>(); break;
+                        case 2: wait_vmcnt<2 * NB>(); break;
+                        default: wait_vmcnt<3 * NB>(); break;
+                        }
                     }
                     // Read the block's DMA'd bytes back before publishing them:
                     // an LDS-DMA write is ordered only for the ISSUING wave's
@@ -1949,9 +1996,10 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     // diagonal: a lane's trajectory switch (in diagonal s) decides which
     // state and source table diagonal s + 1 reads.
     // the kept block's outputs (keep_of: VGPRs, one block per W)
-    v4u kr[keep_of<W>() ? uw_of<W>() : 1];
+    constexpr int KN = keep_of<W>() ? keep_n_of<W>() : 1;  // kept diagonals of the block
+    v4u kr[KN];
 #pragma unroll
-    for (int u = 0; u < (keep_of<W>() ? uw_of<W>() : 1); ++u) kr[u] = v4u{0u, 0u, 0u, 0u};
+    for (int u = 0; u < KN; ++u) kr[u] = v4u{0u, 0u, 0u, 0u};
     auto run_block = [&](auto tag, const int sb, auto keep_tag) {
         // KEEP: the kept block -- previous states from kr once the first W
         // diagonals are past (before that the loader read them), outputs to kr
@@ -2002,18 +2050,19 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 // through the loader's window (once per launch)
                 if (!reg_ok) {
 #pragma unroll
-                    for (int u = 0; u < U; ++u) kr[u] = lds_ld(b.wb + u * kWave);
+                    for (int u = 0; u < KN; ++u) kr[u] = lds_ld(b.wb + u * kWave);
                 }
             }
             // (KEEP: the previous state is kr[u], not loaded into In)
             auto fb = [&](int u) -> In {
                 if constexpr (KEEP) {
-                    In in = fetch_b_nx(b, u);
-                    in.xs = kr[u];
-                    return in;
-                } else {
-                    return fetch_b(b, u);
+                    if (u < KN) {
+                        In in = fetch_b_nx(b, u);
+                        in.xs = kr[u < KN ? u : 0];
+                        return in;
+                    }
                 }
+                return fetch_b(b, u);
             };
             In a0 = fb(0), a1 = fb(1);
 #pragma unroll
@@ -2021,7 +2070,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 In nx;
                 if (u + 2 < U) nx = fb(u + 2);
                 const v4u o = diagonal(tag, sb + u, u, a0);
-                if constexpr (KEEP) kr[u] = o;
+                if constexpr (KEEP) {
+                    if (u < KN) kr[u < KN ? u : 0] = o;
+                }
                 a0 = a1;
                 if (u + 2 < U) a1 = nx;
             }
