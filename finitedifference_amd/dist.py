@@ -230,7 +230,7 @@ def create_npy(path, m, ncols):
         f.truncate(len(hdr) + 8 * m * ncols)
 
 
-def _agree(dist, err):
+def agree(dist, err):
     """Every rank learns whether any rank failed: (first error message or
     None).  Collective."""
     msgs = [None] * dist.get_world_size()
@@ -253,7 +253,7 @@ def slabs_to_npy(ctx, w0, num_steps, path, snap_every, dist, rank, world):
             create_npy(path, 2 * nx * ny, ncols)
         except OSError as e:
             err = e
-    bad = _agree(dist, err)
+    bad = agree(dist, err)
     if bad:
         raise RuntimeError(f"snapshot file {path}: {bad}")
     st = None
@@ -262,7 +262,7 @@ def slabs_to_npy(ctx, w0, num_steps, path, snap_every, dist, rank, world):
                             snap_every=snap_every, flags=NPY_GLOBAL | NPY_EXISTING)
     except Exception as e:  # noqa: BLE001  (agreed on below, re-raised on every rank)
         err = e
-    bad = _agree(dist, err)
+    bad = agree(dist, err)
     if bad:
         drop_job_context(ctx)
         if rank == 0 and os.path.exists(path):
@@ -274,7 +274,8 @@ def slabs_to_npy(ctx, w0, num_steps, path, snap_every, dist, rank, world):
 
 def shared_tmp_path(dist, rank, suffix=".npy"):
     """A fresh path every rank of the job agrees on, in BURG_SNAP_DIR or the
-    temporary directory (the ranks of one node share it)."""
+    temporary directory: the ranks must share that directory (one node, as
+    the slabs' halo rings require: POSIX shared memory and IPC handles)."""
     box = [None]
     if rank == 0:
         d = os.environ.get("BURG_SNAP_DIR") or tempfile.gettempdir()

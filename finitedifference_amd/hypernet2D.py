@@ -37,7 +37,7 @@ import numpy as np
 import scipy.sparse as sp
 from scipy.sparse.linalg import LinearOperator
 
-from .dist import job, job_context, job_device, shared_tmp_path, slabs_to_npy
+from .dist import agree, job, job_context, job_device, shared_tmp_path, slabs_to_npy
 from .grid import fom_coefficients, make_2D_grid  # noqa: F401  (re-export)
 from .solver import DEFAULT_TOL, get_context
 from .ecsw import (compute_ECSW_training_matrix_2D_gp,  # noqa: F401  (re-export)
@@ -176,10 +176,16 @@ def _implicit2D_job(d, rank, world, grid_x, grid_y, w0, dt, num_steps, mu, *, so
     path = shared_tmp_path(d, rank)
     st = slabs_to_npy(ctx, np.asarray(w0, dtype=np.float64).ravel(), int(num_steps), path,
                       int(snap_every), d, rank, world)
-    snaps = np.load(path, mmap_mode="c")
-    d.barrier()  # every rank holds its map: the name can go
+    snaps, err = None, None
+    try:
+        snaps = np.load(path, mmap_mode="c")
+    except Exception as e:  # noqa: BLE001  (agreed on below: no rank waits for one that failed)
+        err = e
+    bad = agree(d, err)  # every rank holds its map (or all raise): the name can go
     if rank == 0:
         os.remove(path)
+    if bad:
+        raise RuntimeError(f"multi-GPU snapshot matrix {path}: {bad}")
     if verbose and rank == 0:
         print("\n".join(" ... Working on timestep {}".format(i) for i in range(int(num_steps))))
     if return_stats:
