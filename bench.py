@@ -108,7 +108,7 @@ def parse():
                          "for the host-side collectives (use small slabs so all ranks' "
                          "workgroups are resident together)")
     ap.add_argument("--pmc-file", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--isa-file", default=os.path.join(ROOT, "profiles", "r05", "pipe_isa.json"))
+    ap.add_argument("--isa-file", default=os.path.join(ROOT, "profiles", "r06", "pipe_isa.json"))
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end field (1024^2 x 500 trajectory + .npy file)")
     return ap.parse_args()

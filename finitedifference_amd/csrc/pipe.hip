@@ -122,6 +122,46 @@ constexpr unsigned G = kPipeGranuleStride;
 #ifndef BURG_AB_SKIP
 #define BURG_AB_SKIP 0
 #endif
+// BURG_AB_PAIR_NORING (A/B ceiling probe, wrong ring contents): the paired
+// kernel issues no ring stores and keeps none of their registers -- what a
+// store wave could at most take off its compute waves (0: off)
+#ifndef BURG_AB_PAIR_NORING
+#define BURG_AB_PAIR_NORING 0
+#endif
+// BURG_AB_PAIR_COAL (A/B probe, wrong ring layout): the paired steady blocks
+// store every lane's cells at lane 0's ring entries (one contiguous 1 KB
+// entry per store instead of ~8 partial ones)
+#ifndef BURG_AB_PAIR_COAL
+#define BURG_AB_PAIR_COAL 0
+#endif
+// BURG_AB_PAIR_OOB (A/B probe, no ring contents): the paired kernel issues
+// its ring stores at out-of-range offsets (dropped by the buffer unit)
+#ifndef BURG_AB_PAIR_OOB
+#define BURG_AB_PAIR_OOB 0
+#endif
+// BURG_AB_PAIR_NOKEEP (A/B probe, store-VGPR hazard unguarded): the paired
+// kernel's ring stores without their kept registers
+#ifndef BURG_AB_PAIR_NOKEEP
+#define BURG_AB_PAIR_NOKEEP 0
+#endif
+// BURG_AB_PAIR_SMALL (A/B probe, wrong ring contents): the paired kernel's
+// ring stores folded into the first 16 KB of each tile's ring (L2-resident)
+#ifndef BURG_AB_PAIR_SMALL
+#define BURG_AB_PAIR_SMALL 0
+#endif
+// BURG_AB_SW_NOSTORE (A/B probe, no ring contents): the store wave of the
+// one-cell W = 16 kernels walks and publishes but issues no stores
+#ifndef BURG_AB_SW_NOSTORE
+#define BURG_AB_SW_NOSTORE 0
+#endif
+// BURG_AB_PAIR_SWEMU (A/B probe, wrong ring contents; with
+// BURG_AB_PAIR_NORING): a store wave for the paired kernel, emulated -- it
+// copies each paired block's 16 LDS slots to 16 ring entries once the
+// compute wave has moved past the block, with no overwrite guard (the traffic
+// and LDS reads of a real one, not its coupling)
+#ifndef BURG_AB_PAIR_SWEMU
+#define BURG_AB_PAIR_SWEMU 0
+#endif
 // BURG_KEEP_BLOCK (round 6): the
 // wide tiles keep the outputs of ONE block of U diagonals per W -- the block
 // at diagonal kKeepS mod W -- in VGPRs of the compute wave, and read the next
@@ -361,9 +401,14 @@ __device__ __forceinline__ void st_sys_so(__amdgpu_buffer_rsrc_t rs, unsigned vo
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
 }
+// (BURG_RING_ST_AUX: A/B probe of the ring stores' cache policy bits; 0 =
+// the default policy)
+#ifndef BURG_RING_ST_AUX
+#define BURG_RING_ST_AUX 0
+#endif
 [[maybe_unused]] __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, BURG_RING_ST_AUX);
 }
 [[maybe_unused]] __device__ __forceinline__ v4u ld_plain(__amdgpu_buffer_rsrc_t rs, unsigned off)
 {
@@ -1005,7 +1050,55 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             // past d's block (prog), and publishes done[k] (diagonals
             // copied), which the compute wave's readiness test waits for
             // before it overwrites a slot (W diagonals later)
+#if BURG_AB_PAIR_SWEMU
+            if constexpr (PAIR) {
+                const int totalb = (8 * K + 8 + kWave - 1 + U - 1) / U * U;
+                const unsigned Lu = (unsigned)a.L;
+                int cp[4] = {0, 0, 0, 0};
+                unsigned pw4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) pw4[k] = (unsigned)a.origin;
+                long long t_prog = now_rt();
+                for (;;) {
+                    bool left = false, any = false;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (k >= nval) continue;
+                        if (cp[k] < totalb && cp[k] + U <= lds_ldi(&sm.prog[k])) {
+                            const __amdgpu_buffer_rsrc_t ring =
+                                rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
+                            unsigned e = pw4[k];
+                            v4u v[2 * U];
+#pragma unroll
+                            for (int u = 0; u < 2 * U; ++u) v[u] = lds_ld(&sm.st[k][u][lane]);
+#pragma unroll
+                            for (int u = 0; u < 2 * U; ++u) {
+                                unsigned o = e * 1024u + lane * 16u;
+                                launder(o);
+                                st_plain(ring, o, v[u]);
+                                e = e + 1 == Lu ? 0u : e + 1;
+                            }
+                            pw4[k] = e;
+                            cp[k] += U;
+                            if (lane == 0) lds_sti(&sm.done[k], cp[k]);
+                            any = true;
+                        }
+                        left |= cp[k] < totalb;
+                    }
+                    if (!left || lds_ldi(&sm.perm[5])) break;
+                    const long long tn = now_rt();
+                    if (any) {
+                        t_prog = tn;
+                    } else {
+                        if (tn - t_prog > a.spin_ticks) break;
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                return;
+            }
+#else
             if constexpr (PAIR) return;  // (the paired kernel stores itself)
+#endif
             // (BURG_STOREWAVE_PRIO: race-screen builds only)
 #ifndef BURG_STOREWAVE_PRIO
 #define BURG_STOREWAVE_PRIO 0
@@ -1052,7 +1145,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                             const int t = cp[k] + u - lane;
                             unsigned o = (unsigned)t < (unsigned)KW ? e * 1024u + lane * 16u : kOOB;
                             launder(o);
+#if !BURG_AB_SW_NOSTORE
                             st_plain(ring, o, v[u]);
+#endif
                             kv[u] = v[u];
                             ko[u] = o;
                             e = (!ret && e + 1 == Lu) ? 0u : e + 1;
@@ -1176,8 +1271,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         v4u kq_a = v4u{0u, 0u, 0u, 0u}, kq_b = kq_a, kq_e = kq_a, kq_na = kq_a, kq_nb = kq_a;
         unsigned kq_ra = 0u, kq_rb = 0u, kq_eo = 0u, kq_oa = 0u, kq_ob = 0u;
         auto keep_prev = [&]() {
+#if BURG_AB_PAIR_NORING || BURG_AB_PAIR_NOKEEP
+            asm volatile("" ::"v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
+#else
             asm volatile("" ::"v"(kq_a), "v"(kq_b), "v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_ra), "v"(kq_rb),
                          "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
+#endif
         };
         // missing inflows / grants of block [sb, sb + 8): name_it = false: any
         // (one ballot); true: the kinds (bits as err[3] >> 8)
@@ -1307,10 +1406,19 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             keep_prev();
             unsigned ra = vA ? eA * 1024u + lane16 : kOOB, rb = vB ? eB * 1024u + lane16 : kOOB;
             v4u ka = outA, kb = outB;
+#if BURG_AB_PAIR_OOB
+            ra = rb = kOOB;
+#endif
+#if BURG_AB_PAIR_SMALL
+            ra &= 0x3FFFu;
+            rb &= 0x3FFFu;
+#endif
+#if !BURG_AB_PAIR_NORING
             launder(ra);
             launder(rb);
             st_plain(ring, ra, ka);
             st_plain(ring, rb, kb);
+#endif
             eA += atE ? 9u : 1u;
             if (eA >= Lu) eA -= Lu;
             // east edge: B's column 15 (step qB)
@@ -1391,7 +1499,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             const unsigned eoff = east_glob ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             // ring: A's entry at diagonal u is eA + u (+ 8 from uw8 on); B's is 8 below
             // (rA*: byte offsets -- not oA*, the cells' outputs below)
+#if BURG_AB_PAIR_COAL
+            const unsigned rA1 = __builtin_amdgcn_readfirstlane(eA) * 1024u + lane16, rA2 = rA1 + 8192u;
+#else
             const unsigned rA1 = eA * 1024u + lane16, rA2 = rA1 + 8192u;
+#endif
             // north (top lane): A at (step, column) = (q0, c0 + u) before uw8, (q0 + 1, c0 + u - 8)
             // after; B one step earlier at column 8 + that
             const bool tl = has_north & (lane == top);
@@ -1456,10 +1568,19 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 keep_prev();
                 unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u, rB = rA - 8192u;
                 v4u ka = outA, kb = outB;
+#if BURG_AB_PAIR_OOB
+                rA = rB = kOOB;
+#endif
+#if BURG_AB_PAIR_SMALL
+                rA &= 0x3FFFu;
+                rB &= 0x3FFFu;
+#endif
+#if !BURG_AB_PAIR_NORING
                 launder(rA);
                 launder(rB);
                 st_plain(ring, rA, ka);
                 st_plain(ring, rB, kb);
+#endif
                 v4u eo = as_v4u(oeB0, oeB1);
                 lds_st(atE ? eaddr : dumpv, eo);
                 unsigned eo_off = atE ? eoff : kOOB;
@@ -1559,6 +1680,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 lds_st(((lane < 16) & (d >= 0) & (d < KW)) ? &sm.ins[k][d & (kNI - 1)] : dumpv, lempty);
             }
         }
+#if BURG_AB_PAIR_SWEMU
+        lds_sti(lane == 0 ? &sm.prog[k] : sink, total2 + U);
+#endif
         if (lane == 0) {
             if (pspins) atomicAdd(&a.stats->stall_spins, pspins);
             if (pslow) atomicAdd(&a.stats->slow_diagonals, pslow);

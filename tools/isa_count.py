@@ -240,7 +240,7 @@ def summarise(run):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r05", "pipe_isa.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r06", "pipe_isa.json"))
     args = ap.parse_args()
     with tempfile.TemporaryDirectory() as d:
         # pipe.hip (wide kernels) and pipe_narrow.hip (narrow), both with
