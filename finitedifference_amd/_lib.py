@@ -243,12 +243,14 @@ def is_default_build():
     return build_flags().endswith("knobs: none")
 
 
-def ring_audit(W, num_steps, snap_every=1, ring_cap=0, paired=False):
+def ring_audit(W, num_steps, snap_every=1, ring_cap=0, paired=False, paired_layout=False):
     """burg_ring_audit_ex as a dict (host-only; no GPU needed); paired: the
-    paired-halves W = 16 kernel's walk."""
+    paired-halves W = 16 kernel's walk; paired_layout (with paired): its store
+    wave's paired sweep layout (BURG_AUDIT_PAIRED_LAYOUT)."""
     rep = (ctypes.c_int64 * 9)()
+    flags = (1 if paired else 0) | (2 if paired_layout else 0)
     check(load().burg_ring_audit_ex(int(W), int(num_steps), int(snap_every), int(ring_cap),
-                                    1 if paired else 0, rep))
+                                    flags, rep))
     keys = ("accesses", "max_entry", "entries_per_tile", "out_of_range", "walk_mismatch",
             "retained_overwritten", "early_overwrite", "retained_states", "snap_every")
     return dict(zip(keys, list(rep)))

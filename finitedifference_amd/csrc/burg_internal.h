@@ -130,6 +130,19 @@ __host__ __device__ inline long long ring_pos(long long s, long long origin, lon
     return d < 0 ? d + L : d;
 }
 
+// The paired sweep layout (pipe.hip's paired kernel with its store wave, in
+// burg_sweep launches): the launch's step t >= 0,
+// column c (0..15) of lane r -- computed at paired diagonal s = 8 t + c + r
+// by half c / 8 -- sits at entry origin + 2 s + c / 8 (mod L), so that the
+// store wave writes each half of a paired diagonal as one contiguous 1 KB
+// entry.  The launch's initial state keeps ring_pos's layout (diagonals -W ..
+// 62), which the kernel reads before it writes any entry.
+__host__ __device__ inline long long ring_pos_paired(long long t, int c, int r, long long origin, long long L)
+{
+    const long long d = (origin + 2 * (8 * t + c + r) + (c >> 3)) % L;
+    return d < 0 ? d + L : d;
+}
+
 // Walk of a tile's diagonals one block of U at a time through the retained
 // windows of ring_pos (a.ret_k > 0): entry of the block's first diagonal,
 // advanced per block without divisions.  The windows, the working ring's
@@ -187,6 +200,7 @@ struct StreamArgs {
     int ret_k, ret_n;    // retained windows (ring_pos): snap_every, windows; 0: plain ring
     long long ret_base;  // entry of window 0
     int K;               // time steps of this launch
+    int play;            // 1: the launch's states (k >= 1) in the paired sweep layout (ring_pos_paired)
     int flags;           // diagnostics only: bit 0 = ignore neighbours (wrong results)
     int nti, ntj, ntiles, R;
     unsigned *err;       // bit 0: a mailbox wait gave up
@@ -241,6 +255,8 @@ struct PipeArgs {
     size_t colc_dstride;
     int wg_cm;            // workgroup order: 1 column-major (tile row fastest), 0 row-major
     int pair;             // W = 16 run kernel with paired 8-column halves (pipe.hip PAIR)
+    unsigned w0c[4];      // paired sweeps with a store wave: the uniform initial state {u0, v0} (bits)
+    int play;             // paired sweeps with a store wave: states in the paired layout (ring_pos_paired)
     long long spin_ticks; // s_memrealtime ticks (100 MHz) a wait may last without progress
     long long census_ticks;  // how long the residency census may wait for the whole grid
     unsigned *err;        // [4]: flag, tile, diagonal/step, which wait (64: residency census)
@@ -285,6 +301,7 @@ int launch_ring_extract(const StreamArgs &a, int W, int k0, int kstep, int count
 bool pipe_width_supported(int W);
 int pipe_block_of(int W);  // diagonals per block of the trajectory kernel
 bool pipe_sweep_width_supported(int W);
+bool pipe_pair_sweep_uniform_only();  // paired sweeps need a uniform initial state (PipeArgs::w0c)
 int pipe_max_resident_blocks(int W, bool sweep = false);
 int launch_pipe(const PipeArgs &a, int W, hipStream_t st);
 int launch_pipe_fill(void *p, size_t n16, int color, hipStream_t st);

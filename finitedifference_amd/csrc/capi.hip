@@ -142,6 +142,12 @@ struct burg_ctx {
     double *d_state[2] = {nullptr, nullptr};
     int cur = 0;
     double *d_w0 = nullptr;  // last uploaded state (burg_trajectory from_initial)
+    // d_w0 uniform (every u equal, every v equal; bitwise) and its {u0, v0}
+    // bits: the paired sweep kernel restarts its trajectories from that
+    // constant (pipe_args, PipeArgs::w0c)
+    bool w0_uni = false;
+    unsigned w0c[4] = {0u, 0u, 0u, 0u};
+    int last_play = 0;  // the last pipe launch wrote the paired sweep layout (ring_pos_paired)
     double *d_r = nullptr, *d_d = nullptr, *d_x = nullptr, *d_partials = nullptr,
            *d_sumsq = nullptr;
     int npartials = 0;
@@ -640,6 +646,16 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
         int pair_opt = e ? std::atoi(e) : -1;
         if (pair_opt < 0) pair_opt = (a.T < K || 2LL * K >= (long long)c->nx + c->nrows) ? 1 : 0;
         a.pair = (pair_opt == 1 || pair_opt == 2) && c->sp.W == 16 && a.ret_k == 0 ? pair_opt : 0;
+        // the paired sweep kernel (with its store wave) restarts trajectories
+        // from a uniform initial state only -- the reference's w0 = 1
+        // (C/run_fom.py:33-35); any other initial state sweeps one-cell
+        if (a.pair && a.colc_b && a.T < K && pipe_pair_sweep_uniform_only() && !c->w0_uni) a.pair = 0;
+        std::memcpy(a.w0c, c->w0c, sizeof a.w0c);
+        // paired sweeps with a store wave write the paired layout
+        // (ring_pos_paired: contiguous 1 KB entries; the sweep's extraction
+        // reads it); BURG_PAIR_LAYOUT=0 keeps the standard one (A/B)
+        const char *pl = std::getenv("BURG_PAIR_LAYOUT");
+        a.play = (a.pair && a.colc_b && pipe_pair_sweep_uniform_only() && !(pl && std::atoi(pl) == 0)) ? 1 : 0;
     }
     a.spin_ticks = c->spin_ticks;
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
@@ -701,6 +717,7 @@ int stream_launch(burg_ctx *c, long long L, long long origin, int K, float *ms,
     HIPCHK(hipEventRecord(c->ev0, c->stream));
     if (pipe) {
         const PipeArgs pa = pipe_args(c, L, origin, K, mp);
+        c->last_play = pa.play;
         CHK(launch_pipe(pa, c->sp.W, c->stream));
         if (pa.pair) ++c->paired_launches;
     } else {
@@ -1797,6 +1814,26 @@ int burg_upload_state(burg_ctx *c, const double *w)
     HIPCHK(h2d(c->d_state[c->cur], w, c->m() * sizeof(double), c->stream));
     if (!c->d_w0)
         if (int e = dalloc(&c->d_w0, c->m())) return e;
+    {
+        // uniform (u plane | v plane each one value, bitwise)? -- the paired
+        // sweep kernel's condition (pipe_args)
+        const size_t n = c->m() / 2;
+        uint64_t u0 = 0, v0 = 0;
+        std::memcpy(&u0, &w[0], 8);
+        std::memcpy(&v0, &w[n], 8);
+        bool uni = true;
+        for (size_t i = 0; i < n && uni; ++i) {
+            uint64_t x, y;
+            std::memcpy(&x, &w[i], 8);
+            std::memcpy(&y, &w[n + i], 8);
+            uni = x == u0 && y == v0;
+        }
+        c->w0_uni = uni;
+        c->w0c[0] = (unsigned)u0;
+        c->w0c[1] = (unsigned)(u0 >> 32);
+        c->w0c[2] = (unsigned)v0;
+        c->w0c[3] = (unsigned)(v0 >> 32);
+    }
     HIPCHK(hipMemcpyAsync(c->d_w0, c->d_state[c->cur], c->m() * sizeof(double),
                           hipMemcpyDeviceToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -2368,7 +2405,8 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
     HIPCHK(hipMemGetInfo(&freeb, &totalb));
     const size_t per_entry = (size_t)c->sp.ntiles * kWave * sizeof(d2);
     const long long Lmax = (long long)(freeb / 3 / per_entry);
-    long long G = (Lmax - W - 96) / ((long long)T * W);
+    // (the paired sweep layout reaches 2 (8 K + 70) + 1 entries: L = K W + 2 W + 128)
+    long long G = (Lmax - 2 * W - 128) / ((long long)T * W);
     G = std::min<long long>(G, nmu);
     G = std::min<long long>(G, stream_max_steps(c) / T);
     G = std::min<long long>(G, narrow ? kPipeSweepMax : 1);
@@ -2380,7 +2418,7 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
         cleanup();
         return fail(BURG_ENOMEM, "not enough device memory for one %d-step trajectory ring", T);
     }
-    const long long L = G * T * W + W + 96;
+    const long long L = G * T * W + 2 * W + 128;
     if ((rc = ensure_ring(c, L))) {
         cleanup();
         return rc;
@@ -2414,6 +2452,9 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
             c->ov_lbc = d_lbcb + (size_t)g0 * c->nrows;
         }
         rc = stream_launch(c, L, 0, nb * T, &ms);
+        // the launch's states as it laid them out (paired sweep layout or not)
+        StreamArgs xa = stream_args(c, L, 0, 0);
+        xa.play = c->last_play;
         c->sw_T = 0;
         c->ov_colc = nullptr;
         c->ov_lbc = nullptr;
@@ -2427,7 +2468,7 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
                 const size_t cap = m * (size_t)out.ld_dev - (size_t)(g0 + j) * ncols;
                 const double *p0 = c->d_w0;
                 if (launch_transpose(&p0, 1, m, dst, (int)out.ld_dev, cap, bflag(c), c->stream) ||
-                    (ncols > 1 && launch_ring_extract(stream_args(c, L, 0, 0), W,
+                    (ncols > 1 && launch_ring_extract(xa, W,
                                                       (int)(j * T + snap_every), snap_every,
                                                       (int)(ncols - 1), dst + 1, (int)out.ld_dev,
                                                       cap - 1, c->stream)))
@@ -2448,7 +2489,7 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
             // columns 1.. = launch states j*T + k*snap_every
             for (int64_t k0 = 1; k0 < ncols; k0 += S) {
                 const int n = (int)std::min<int64_t>(S, ncols - k0);
-                if (launch_ring_extract(stream_args(c, L, 0, 0), W,
+                if (launch_ring_extract(xa, W,
                                         (int)(j * T + k0 * snap_every), snap_every, n, d_tr, n,
                                         (size_t)S * m, c->stream) ||
                     d2h_2d(dst + k0, (size_t)ld_snaps * sizeof(double), d_tr,
@@ -2466,7 +2507,9 @@ static int sweep_impl(burg_ctx *c, int nmu, const double *src_b, const double *l
     }
     if (rc == BURG_OK) {
         // the last trajectory's final state becomes the resident state
-        rc = launch_ring_extract(stream_args(c, L, 0, 0), W, last_nb * T, 1, 1,
+        StreamArgs fa = stream_args(c, L, 0, 0);
+        fa.play = c->last_play;
+        rc = launch_ring_extract(fa, W, last_nb * T, 1, 1,
                                  c->d_state[c->cur ^ 1], 1, m, c->stream);
         if (rc) rc = fail(BURG_EHIP, "ring extract launch failed");
         else c->cur ^= 1;
@@ -3419,8 +3462,11 @@ int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int f
     if (!pipe_width_supported(W)) return fail(BURG_EINVAL, "W=%d: not a pipe-engine width", W);
     if (num_steps < 1 || snap_every < 1 || ring_cap < 0)
         return fail(BURG_EINVAL, "num_steps, snap_every >= 1, ring_cap >= 0");
-    if (flags & ~BURG_AUDIT_PAIRED) return fail(BURG_EINVAL, "unknown flags %#x", flags);
+    if (flags & ~(BURG_AUDIT_PAIRED | BURG_AUDIT_PAIRED_LAYOUT)) return fail(BURG_EINVAL, "unknown flags %#x", flags);
     const bool paired = (flags & BURG_AUDIT_PAIRED) != 0;
+    const bool play = (flags & BURG_AUDIT_PAIRED_LAYOUT) != 0;
+    if (play && (!paired || snap_every != 1 || ring_cap != 0))
+        return fail(BURG_EINVAL, "the paired sweep layout: BURG_AUDIT_PAIRED, snap_every 1, no ring cap");
     // (the paired-halves kernel: W = 16, plain rings -- pipe_args)
     if (paired && (W != 16 || (snap_every >= 2 && snap_every * W >= W + 64)))
         return fail(BURG_EINVAL, "the paired walk runs W = 16 on plain rings only");
@@ -3438,7 +3484,7 @@ int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int f
         if (ring_cap > 0) C = std::min<long long>(C, ring_cap);
         K = std::min<long long>(num_steps, std::max<long long>(C, ((1 << 21) - 4096) / W - 1));
         mp = TrajMap{};
-        mp.L = C * W + W + 96;
+        mp.L = play ? K * W + 2 * W + 128 : C * W + W + 96;  // (play: sweep_impl's ring)
         mp.Lt = ring_stride(mp.L);
     }
     struct RA {
@@ -3494,7 +3540,32 @@ int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int f
             e0l %= mp.L;
             eA[lane] = (unsigned)(e0l < 0 ? e0l + mp.L : e0l);
         }
-        for (long long sb = 0; sb < total2; sb += 8) {
+        for (long long sb = 0; sb < total2 && play; sb += 8) {
+            // the store wave's paired sweep layout: the block's halves of
+            // diagonal sb + u at entries origin + 2 (sb + u) and + 1
+            unsigned ep = (unsigned)((mp.origin + 2 * sb) % mp.L);
+            for (int u = 0; u < 8; ++u) {
+                const unsigned ep1 = ep + 1u == Lu ? 0u : ep + 1u;
+                for (int lane = 0; lane < kWave; ++lane) {
+                    const long long tau = sb + u - lane;
+                    const long long cA = tau & 7, qA = tau >> 3;
+                    const bool vA = tau >= 0 && tau < K8, vB = tau >= 8 && tau - 8 < K8;
+                    const long long dA = 16 * qA + cA + lane, dB = dA - 8;  // (cell ids: standard diagonals)
+                    if (vA) {
+                        chk(ep, dA, false);
+                        if ((long long)ep != ring_pos_paired(qA, (int)cA, lane, mp.origin, mp.L)) ++mism;
+                        write(ep, dA, lane);
+                    }
+                    if (vB) {
+                        chk(ep1, dB, false);
+                        if ((long long)ep1 != ring_pos_paired(qA - 1, (int)(8 + cA), lane, mp.origin, mp.L)) ++mism;
+                        write(ep1, dB, lane);
+                    }
+                }
+                ep = ep1 + 1u == Lu ? 0u : ep1 + 1u;
+            }
+        }
+        for (long long sb = 0; sb < total2 && !play; sb += 8) {
             // the kernel's steady test (a full strip assumed), wave-uniform
             bool steady = sb >= 72 && sb + 8 <= K8;
             for (int lane = 0; lane < kWave && steady; ++lane)
@@ -3575,7 +3646,9 @@ int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int f
     // the retained states (burg_trajectory_copy -> ring_extract_kernel): every
     // cell must still hold the diagonal that produced it
     std::vector<long long> states;
-    if (ret) {
+    if (play) {
+        for (long long q = 1; q <= K; ++q) states.push_back(q);  // (state 0: the uploaded w0)
+    } else if (ret) {
         for (int j = 1; j <= mp.n; ++j) states.push_back((long long)j * k);  // (state 0: d_ret0)
     } else {
         long long r0 = 0;
@@ -3587,7 +3660,7 @@ int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int f
         for (int lane = 0; lane < kWave; ++lane)
             for (int cl = 0; cl < W; ++cl) {
                 const long long s = (q - 1) * W + cl + lane;
-                const long long e = pos(s);
+                const long long e = play ? ring_pos_paired(q - 1, cl, lane, mp.origin, mp.L) : pos(s);
                 chk(e, s, false);
                 if (e >= 0 && e < Lt && cell[(size_t)e * kWave + lane] != s) ++over;
             }

@@ -82,6 +82,7 @@
 namespace burg {
 const void *pipe_narrow_fn(int W, bool sweep);  // pipe_narrow.hip
 const void *pipe_pair_fn(bool sweep);           // pipe_narrow.hip: pipe_kernel<16, sweep, true>
+size_t pipe_pair_image(bool sweep);             // pipe_narrow.hip: its LDS image
 namespace {
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -121,46 +122,6 @@ constexpr unsigned G = kPipeGranuleStride;
 // wide tiles whose previous states the loader does not read back (0: off)
 #ifndef BURG_AB_SKIP
 #define BURG_AB_SKIP 0
-#endif
-// BURG_AB_PAIR_NORING (A/B ceiling probe, wrong ring contents): the paired
-// kernel issues no ring stores and keeps none of their registers -- what a
-// store wave could at most take off its compute waves (0: off)
-#ifndef BURG_AB_PAIR_NORING
-#define BURG_AB_PAIR_NORING 0
-#endif
-// BURG_AB_PAIR_COAL (A/B probe, wrong ring layout): the paired steady blocks
-// store every lane's cells at lane 0's ring entries (one contiguous 1 KB
-// entry per store instead of ~8 partial ones)
-#ifndef BURG_AB_PAIR_COAL
-#define BURG_AB_PAIR_COAL 0
-#endif
-// BURG_AB_PAIR_OOB (A/B probe, no ring contents): the paired kernel issues
-// its ring stores at out-of-range offsets (dropped by the buffer unit)
-#ifndef BURG_AB_PAIR_OOB
-#define BURG_AB_PAIR_OOB 0
-#endif
-// BURG_AB_PAIR_NOKEEP (A/B probe, store-VGPR hazard unguarded): the paired
-// kernel's ring stores without their kept registers
-#ifndef BURG_AB_PAIR_NOKEEP
-#define BURG_AB_PAIR_NOKEEP 0
-#endif
-// BURG_AB_PAIR_SMALL (A/B probe, wrong ring contents): the paired kernel's
-// ring stores folded into the first 16 KB of each tile's ring (L2-resident)
-#ifndef BURG_AB_PAIR_SMALL
-#define BURG_AB_PAIR_SMALL 0
-#endif
-// BURG_AB_SW_NOSTORE (A/B probe, no ring contents): the store wave of the
-// one-cell W = 16 kernels walks and publishes but issues no stores
-#ifndef BURG_AB_SW_NOSTORE
-#define BURG_AB_SW_NOSTORE 0
-#endif
-// BURG_AB_PAIR_SWEMU (A/B probe, wrong ring contents; with
-// BURG_AB_PAIR_NORING): a store wave for the paired kernel, emulated -- it
-// copies each paired block's 16 LDS slots to 16 ring entries once the
-// compute wave has moved past the block, with no overwrite guard (the traffic
-// and LDS reads of a real one, not its coupling)
-#ifndef BURG_AB_PAIR_SWEMU
-#define BURG_AB_PAIR_SWEMU 0
 #endif
 // BURG_KEEP_BLOCK (round 6): the
 // wide tiles keep the outputs of ONE block of U diagonals per W -- the block
@@ -401,14 +362,9 @@ __device__ __forceinline__ void st_sys_so(__amdgpu_buffer_rsrc_t rs, unsigned vo
 {
     __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, soff, 0);
 }
-// (BURG_RING_ST_AUX: A/B probe of the ring stores' cache policy bits; 0 =
-// the default policy)
-#ifndef BURG_RING_ST_AUX
-#define BURG_RING_ST_AUX 0
-#endif
 [[maybe_unused]] __device__ __forceinline__ void st_plain(__amdgpu_buffer_rsrc_t rs, unsigned off, v4u v)
 {
-    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, BURG_RING_ST_AUX);
+    __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, 0);
 }
 [[maybe_unused]] __device__ __forceinline__ v4u ld_plain(__amdgpu_buffer_rsrc_t rs, unsigned off)
 {
@@ -494,11 +450,15 @@ template <int W, bool SWEEP>
 constexpr int src_pad_of() { return (!is_wide<W>() && SWEEP) ? BURG_NARROW_U : 0; }
 
 // LDS image of one workgroup (SWEEP: a parameter sweep, burg_sweep -- the
-// initial state and every trajectory's source / inlet terms stay on chip)
-template <int W, bool SWEEP>
+// initial state and every trajectory's source / inlet terms stay on chip;
+// PSW: the paired kernel with its store wave, DESIGN.md section 4.1g --
+// two state slots per paired diagonal and half, and no st0: its sweeps start
+// every trajectory from a uniform initial state, a constant)
+template <int W, bool SWEEP, bool PSW = false>
 struct PipeLds {
     static constexpr bool WIDE = is_wide<W>();
     static constexpr int kSW = SWEEP ? kPipeSweepMax : 1;
+    static constexpr bool ST0 = SWEEP && !PSW;
     // wide: previous states by diagonal, filled by LDS-DMA (M0 base + 16 B
     // per lane) -- first in the image; the DMA reaches every byte of the
     // CU's LDS, not only the 64 KB below 2^16 (tools/probes/dma_high_probe.hip
@@ -506,8 +466,10 @@ struct PipeLds {
     // (narrow tiles: unused by the window; its 8 entries hold the zero south
     // inflow of a boundary strip, read by block offsets -- see zeros)
     v4u win[WIDE ? 4 : 1][WIDE ? win_of<W>() : 1][WIDE ? kWave : BURG_NARROW_U];
-    v4u st[4][WIDE ? 1 : W][WIDE ? 1 : kWave];     // narrow: the lane's outputs of the last W diagonals
-    v4u st0[4][SWEEP ? W : 1][SWEEP ? kWave : 1];  // sweep: initial state, st's layout
+    // narrow: the lane's outputs of the last W diagonals (PSW: 2 W -- the
+    // paired diagonal's A output in slot s mod 16, B's in 16 + s mod 16)
+    v4u st[4][WIDE ? 1 : (PSW ? 2 * W : W)][WIDE ? 1 : kWave];
+    v4u st0[4][ST0 ? W : 1][ST0 ? kWave : 1];  // sweep: initial state, st's layout
     double srcb[kSW][4][SWEEP ? W + src_pad_of<W, SWEEP>() : 1];  // sweep: src of trajectory j, by column
     double lbt[kSW][SWEEP ? kWave : 1];            // sweep: inlet term of trajectory j, by row
     // per wave: {hx, src} of the tile's columns, + the first kPad again, so a
@@ -557,18 +519,21 @@ template <int W, bool SWEEP, bool PAIR = false>
 __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu(min_waves_of<W, SWEEP>()))) void pipe_kernel(PipeArgs a)
 {
     constexpr int kThreads = threads_of<W>();
+    // the paired kernel with a store wave: its
+    // compute waves issue no ring stores
+    constexpr bool PSW = PAIR && store_wave_of<W>();
+    using Img = PipeLds<W, SWEEP, PSW>;
     static_assert(win_of<W>() % uw_of<W>() == 0, "the window holds whole blocks");
-    static_assert(sizeof(PipeLds<W, SWEEP>) <= 160 * 1024, "LDS image exceeds the CU's 160 KiB");
+    static_assert(sizeof(Img) <= 160 * 1024, "LDS image exceeds the CU's 160 KiB");
     // the LDS-DMA window sits at the image's start and ends below the range
     // the probe verified (tools/probes/dma_high_probe.hip: 0 .. 160 KB)
-    using Img = PipeLds<W, SWEEP>;
     static_assert(offsetof(Img, win) == 0 && sizeof(Img::win) <= 160 * 1024,
                   "LDS-DMA window outside the probed range");
     static_assert(!(u16_of<W>() && two_per_cu<W>()), "blocks of 16 need the whole CU's LDS");
     constexpr bool WIDE = is_wide<W>();
     // three narrow W=8 workgroups per CU: room for 8 slab processes sharing one
     // GPU (the 750^2 C5 case, tests/test_gpu_parity.py) with all grids resident
-    static_assert(W != 8 || SWEEP || 3 * sizeof(PipeLds<W, SWEEP>) <= 160 * 1024,
+    static_assert(W != 8 || SWEEP || 3 * sizeof(Img) <= 160 * 1024,
                   "narrow W=8 LDS image must fit three times in a CU");
     static_assert(W == 8 || W == 16 || (WIDE && W <= 1024 && (W & (W - 1)) == 0),
                   "pipe engine: W in {8, 16, 32, ..., 1024}");
@@ -581,7 +546,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     constexpr int kNI = ni_of<W, SWEEP>();
     constexpr int kRL = rl_of<W>();
     constexpr int kLA = la_of<W>();
-    LDS PipeLds<W, SWEEP> &sm = *(LDS PipeLds<W, SWEEP> *)pipe_lds_image;
+    LDS Img &sm = *(LDS Img *)pipe_lds_image;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     const int wg = blockIdx.x;
@@ -677,7 +642,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
     if (wave < nval) {
         const int tile = ti * ntj + tj0 + wave;
         // (the rolling window starts with the columns of t = 0 .. kCCW - 1)
-        for (int c = lane; c < ccn_of<W>() + PipeLds<W, SWEEP>::kPad; c += kWave) {
+        for (int c = lane; c < ccn_of<W>() + Img::kPad; c += kWave) {
             const d2 v = colc_d[(size_t)(tj0 + wave) * W + (c & (ccn_of<W>() - 1))];
             sm.cc[wave][c] = as_v4u(v.x, v.y);
         }
@@ -688,10 +653,14 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             for (int c = 0; c < W; ++c) {
                 const long long e = ring_pos(c + lane - W, a.origin, a.L, W, a.ret_k, a.ret_n, a.ret_base);
                 const v4u x0 = ld_plain(ring, (unsigned)e * 1024u + lane * 16u);
-                // (PAIR: half A in slots 0-7, half B in 8-15, slot (c + lane) mod 8)
-                const int slot = PAIR ? ((c & 8) | ((c + lane) & 7)) : ((c + lane) & (W - 1));
+                // (PAIR: half A in slots 0-7, half B in 8-15, slot (c + lane) mod 8;
+                // PSW: A's column c read at paired diagonal c + lane from slot
+                // (c + lane + 8) mod 16, B's column 8 + c at c + lane + 8 from
+                // slot 16 + (c + lane) mod 16)
+                const int slot = PSW ? ((c < 8) ? ((c + lane + 8) & 15) : 16 + ((c - 8 + lane) & 15))
+                                     : PAIR ? ((c & 8) | ((c + lane) & 7)) : ((c + lane) & (W - 1));
                 sm.st[wave][slot][lane] = x0;
-                if constexpr (SWEEP) sm.st0[wave][slot][lane] = x0;
+                if constexpr (Img::ST0) sm.st0[wave][slot][lane] = x0;
             }
         }
     }
@@ -1050,60 +1019,136 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             // past d's block (prog), and publishes done[k] (diagonals
             // copied), which the compute wave's readiness test waits for
             // before it overwrites a slot (W diagonals later)
-#if BURG_AB_PAIR_SWEMU
-            if constexpr (PAIR) {
-                const int totalb = (8 * K + 8 + kWave - 1 + U - 1) / U * U;
-                const unsigned Lu = (unsigned)a.L;
-                int cp[4] = {0, 0, 0, 0};
-                unsigned pw4[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k) pw4[k] = (unsigned)a.origin;
-                long long t_prog = now_rt();
-                for (;;) {
-                    bool left = false, any = false;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        if (k >= nval) continue;
-                        if (cp[k] < totalb && cp[k] + U <= lds_ldi(&sm.prog[k])) {
-                            const __amdgpu_buffer_rsrc_t ring =
-                                rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
-                            unsigned e = pw4[k];
-                            v4u v[2 * U];
-#pragma unroll
-                            for (int u = 0; u < 2 * U; ++u) v[u] = lds_ld(&sm.st[k][u][lane]);
-#pragma unroll
-                            for (int u = 0; u < 2 * U; ++u) {
-                                unsigned o = e * 1024u + lane * 16u;
-                                launder(o);
-                                st_plain(ring, o, v[u]);
-                                e = e + 1 == Lu ? 0u : e + 1;
-                            }
-                            pw4[k] = e;
-                            cp[k] += U;
-                            if (lane == 0) lds_sti(&sm.done[k], cp[k]);
-                            any = true;
-                        }
-                        left |= cp[k] < totalb;
-                    }
-                    if (!left || lds_ldi(&sm.perm[5])) break;
-                    const long long tn = now_rt();
-                    if (any) {
-                        t_prog = tn;
-                    } else {
-                        if (tn - t_prog > a.spin_ticks) break;
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                return;
-            }
-#else
-            if constexpr (PAIR) return;  // (the paired kernel stores itself)
-#endif
             // (BURG_STOREWAVE_PRIO: race-screen builds only)
 #ifndef BURG_STOREWAVE_PRIO
 #define BURG_STOREWAVE_PRIO 0
 #endif
             __builtin_amdgcn_s_setprio(BURG_STOREWAVE_PRIO);
+            if constexpr (PAIR) {
+                // paired kernel (PSW): block [sb, sb + 8) of compute wave k left
+                // its A outputs in slots (sb & 8) + u and its B outputs in
+                // 16 + (sb & 8) + u.  Sweeps (a.play): each half of paired
+                // diagonal s goes to ONE contiguous entry, origin + 2 s (+ 1
+                // for B) -- ring_pos_paired, burg_internal.h; a full block
+                // without a wrap is 16 stores at a lane offset plus a scalar
+                // entry offset.  Otherwise the standard W = 16 layout, per
+                // lane: the walk the paired compute waves stored along before
+                // (A at eA: +1 per paired diagonal, +9 past column 7; B at
+                // eA - 8).  Cells outside the launch are not stored (A:
+                // 0 <= tau < 8 K, B: 8 <= tau < 8 K + 8; tau = sb + u - lane).
+                // Store VGPRs: waves k = 0, 2 copy
+                // through array x, k = 1, 3 through y, and the wave drains its
+                // stores (vmcnt(0)) before it reloads either -- at k = 2 and at
+                // the end of a pass -- with both arrays kept live until then.
+                const int K8 = 8 * K;
+                const int totalb = (K8 + 8 + kWave - 1 + U - 1) / U * U;
+                const unsigned Lu = (unsigned)a.L;
+                const bool play = a.play != 0;
+                const unsigned lane16 = lane * 16u;
+                int cp[4] = {0, 0, 0, 0};
+                long long e0l = (long long)a.origin + 16LL * ((-lane) >> 3) + ((-lane) & 7) + lane;
+                e0l %= a.L;
+                if (e0l < 0) e0l += a.L;
+                unsigned eA4[4];  // standard walk, per lane
+                unsigned ep4[4];  // paired layout: entry origin + 2 cp (mod L), uniform
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    eA4[k] = (unsigned)e0l;
+                    ep4[k] = (unsigned)a.origin;
+                }
+                static_assert(U == 8, "paired store wave: blocks of 8");
+                auto keep = [](const v4u (&v)[2 * U], const unsigned (&o)[2 * U]) {
+                    asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]),
+                                 "v"(v[7]));
+                    asm volatile("" ::"v"(v[8]), "v"(v[9]), "v"(v[10]), "v"(v[11]), "v"(v[12]), "v"(v[13]),
+                                 "v"(v[14]), "v"(v[15]));
+                    asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "v"(o[5]), "v"(o[6]),
+                                 "v"(o[7]), "v"(o[8]), "v"(o[9]), "v"(o[10]), "v"(o[11]), "v"(o[12]), "v"(o[13]),
+                                 "v"(o[14]), "v"(o[15]));
+                };
+                long long t_prog = now_rt();
+                for (;;) {
+                    bool left = false, any = false;
+                    v4u x[2 * U], y[2 * U];
+                    unsigned ox[2 * U], oy[2 * U];  // (per-lane offsets: the standard walk's slow path)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        if (k == 2) {
+                            // (k = 0's and 1's stores complete before x, y are reloaded)
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                            keep(x, ox);
+                            keep(y, oy);
+                        }
+                        v4u(&v)[2 * U] = (k & 1) ? y : x;
+                        unsigned(&o)[2 * U] = (k & 1) ? oy : ox;
+                        if (k >= nval) continue;
+                        if (cp[k] < totalb && cp[k] + U <= lds_ldi(&sm.prog[k])) {
+                            const __amdgpu_buffer_rsrc_t ring =
+                                rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
+                            const int sb = cp[k], base = sb & 8;
+#pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                v[u] = lds_ld(&sm.st[k][base + u][lane]);
+                                v[U + u] = lds_ld(&sm.st[k][16 + base + u][lane]);
+                            }
+                            const unsigned ep = ep4[k];
+                            if (play && sb >= 72 && sb + U <= K8 && ep + 2u * U <= Lu) {
+                                // full block, no wrap: entries ep + 2 u (A), + 1 (B)
+#pragma unroll
+                                for (int u = 0; u < U; ++u) {
+                                    st_plain_so(ring, lane16, (ep + 2u * u) * 1024u, v[u]);
+                                    st_plain_so(ring, lane16, (ep + 2u * u + 1u) * 1024u, v[U + u]);
+                                }
+                            } else if (play) {
+                                // ramp, tail or wrap: the cells inside the launch
+                                // (exec-masked; the lane offset stays unwritten)
+                                unsigned eq = ep;
+#pragma unroll
+                                for (int u = 0; u < U; ++u) {
+                                    const int tau = sb + u - lane;
+                                    const unsigned eq1 = eq + 1u == Lu ? 0u : eq + 1u;
+                                    if ((unsigned)tau < (unsigned)K8) st_plain_so(ring, lane16, eq * 1024u, v[u]);
+                                    if ((unsigned)(tau - 8) < (unsigned)K8) st_plain_so(ring, lane16, eq1 * 1024u, v[U + u]);
+                                    eq = eq1 + 1u == Lu ? 0u : eq1 + 1u;
+                                }
+                            } else {
+                                unsigned e = eA4[k];
+#pragma unroll
+                                for (int u = 0; u < U; ++u) {
+                                    const int tau = sb + u - lane;
+                                    const unsigned eB = e >= 8u ? e - 8u : e + Lu - 8u;
+                                    o[u] = (unsigned)tau < (unsigned)K8 ? e * 1024u + lane16 : kOOB;
+                                    o[U + u] = (unsigned)(tau - 8) < (unsigned)K8 ? eB * 1024u + lane16 : kOOB;
+                                    st_plain(ring, o[u], v[u]);
+                                    st_plain(ring, o[U + u], v[U + u]);
+                                    e += (tau & 7) == 7 ? 9u : 1u;
+                                    if (e >= Lu) e -= Lu;
+                                }
+                                eA4[k] = e;
+                            }
+                            ep4[k] = ep + 2u * U >= Lu ? ep + 2u * U - Lu : ep + 2u * U;
+                            cp[k] += U;
+                            // (the slots' reads have returned -- the stores used
+                            // them -- so the compute wave may overwrite them)
+                            if (lane == 0) lds_sti(&sm.done[k], cp[k]);
+                            any = true;
+                        }
+                        left |= cp[k] < totalb;
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    keep(x, ox);
+                    keep(y, oy);
+                    if (!left || lds_ldi(&sm.perm[5])) break;
+                    const long long tn = now_rt();
+                    if (any) {
+                        t_prog = tn;
+                    } else {
+                        if (tn - t_prog > a.spin_ticks) break;  // (the compute waves time out themselves)
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                return;
+            }
             const int totalb = (KW + kWave - 1 + U - 1) / U * U;
             const unsigned Lu = (unsigned)a.L;
             int cp[4] = {0, 0, 0, 0};
@@ -1145,9 +1190,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                             const int t = cp[k] + u - lane;
                             unsigned o = (unsigned)t < (unsigned)KW ? e * 1024u + lane * 16u : kOOB;
                             launder(o);
-#if !BURG_AB_SW_NOSTORE
                             st_plain(ring, o, v[u]);
-#endif
                             kv[u] = v[u];
                             ko[u] = o;
                             e = (!ret && e + 1 == Lu) ? 0u : e + 1;
@@ -1241,12 +1284,15 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // of the same step), else its own.  South: lane r - 1's north outflow
         // of the previous diagonal (lane 0: the south inbox, stream index
         // 16 step + column).  Previous states: LDS slot s mod 8 (A) and 8 +
-        // s mod 8 (B), written 8 paired diagonals earlier.  The ring keeps
-        // the standard W = 16 layout (extraction unchanged): the A cell of
-        // (step q, column c) at diagonal 16 q + c + r, per lane.
+        // s mod 8 (B), written 8 paired diagonals earlier (PSW: written to
+        // slots s mod 16 and 16 + s mod 16, read 8 diagonals later from
+        // the other half -- the store wave copies a block out while the
+        // next one runs).  The ring keeps the standard W = 16 layout
+        // (extraction unchanged): the A cell of (step q, column c) at
+        // diagonal 16 q + c + r, per lane.
         static_assert(W == 16 && U == 8, "paired halves: W = 16, blocks of 8");
-        LDS int *const sink = (LDS int *)&sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
-        LDS v4u *const dumpv = &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
+        LDS int *const sink = (LDS int *)&sm.dump[lane & (Img::kDump - 1)];
+        LDS v4u *const dumpv = &sm.dump[lane & (Img::kDump - 1)];
         const int K8 = 8 * K;
         const int total2 = K8 + 8 + kWave - 1;  // lane 63's B cell ends at local time 8K + 7
         long long e0l = (long long)a.origin + 16LL * ((-lane) >> 3) + ((-lane) & 7) + lane;
@@ -1258,7 +1304,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // sweeps: each half's trajectory (B trails A by one step, so it
         // switches to the next trajectory 8 diagonals later): inlet terms,
         // source rows, first step of the next trajectory (its W columns read
-        // the initial state st0)
+        // the initial state: st0, or PSW the uniform initial state w0c)
         // (B is never at the domain's column 0: no inlet term of its own)
         double lbA = lb, lbA_next = lb_next;
         int qnA = qn, qnB = qn, jlA = 0, jlB = 0;
@@ -1271,13 +1317,13 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         v4u kq_a = v4u{0u, 0u, 0u, 0u}, kq_b = kq_a, kq_e = kq_a, kq_na = kq_a, kq_nb = kq_a;
         unsigned kq_ra = 0u, kq_rb = 0u, kq_eo = 0u, kq_oa = 0u, kq_ob = 0u;
         auto keep_prev = [&]() {
-#if BURG_AB_PAIR_NORING || BURG_AB_PAIR_NOKEEP
-            asm volatile("" ::"v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
-#else
-            asm volatile("" ::"v"(kq_a), "v"(kq_b), "v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_ra), "v"(kq_rb),
-                         "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
-#endif
+            if constexpr (PSW)
+                asm volatile("" ::"v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
+            else
+                asm volatile("" ::"v"(kq_a), "v"(kq_b), "v"(kq_e), "v"(kq_na), "v"(kq_nb), "v"(kq_ra), "v"(kq_rb),
+                             "v"(kq_eo), "v"(kq_oa), "v"(kq_ob));
         };
+        const v4u w0c = v4u{a.w0c[0], a.w0c[1], a.w0c[2], a.w0c[3]};  // (PSW sweeps)
         // missing inflows / grants of block [sb, sb + 8): name_it = false: any
         // (one ballot); true: the kinds (bits as err[3] >> 8)
         auto missing2 = [&](int sb, bool name_it) -> unsigned {
@@ -1299,9 +1345,12 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             const int tt = min(sb + 7 - top, K8 + 7);  // the top lane's last local time in the block
             const int th = min(16 * (tt >> 3) + (tt & 7) - (tt >= K8 ? 8 : 0), KW - 1);
             const bool miss_n = has_north & (tt >= 0) & (th >= pn);
+            // PSW: the block overwrites the slots of block sb - 16: copied out?
+            const bool miss_sw = PSW && lds_ldi(&sm.done[k]) < sb - 8;
             if (!name_it)
-                return __builtin_amdgcn_ballot_w64(miss_w | miss_s | miss_el | miss_eg | miss_n) != 0;
+                return (__builtin_amdgcn_ballot_w64(miss_w | miss_s | miss_el | miss_eg | miss_n) != 0) | miss_sw;
             unsigned why = 0;
+            if (miss_sw) why |= 64u;
             if (any_lane(miss_w)) why |= 1u;
             if (any_lane(miss_s)) why |= 2u;
             if (any_lane(miss_el)) why |= 4u;
@@ -1317,16 +1366,22 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             In2 in;
             const int tau = s - lane;
             const int cA = tau & 7, qA = tau >> 3;
-            const int sl = s & 7;
+            // previous states: slot s mod 8 (PSW: the other half's, (s mod 16) ^ 8)
+            const int rA = PSW ? ((s & 15) ^ 8) : (s & 7), rB = (PSW ? 16 : 8) + rA;
             if constexpr (SWEEP) {
                 const bool ntA = qA >= qnA, ntB = qA - 1 >= qnB;
-                in.xa = (ntA ? my_st0 : my_st)[sl * kWave + lane];
-                in.xb = (ntB ? my_st0 : my_st)[(8 + sl) * kWave + lane];
+                if constexpr (PSW) {
+                    in.xa = ntA ? w0c : my_st[rA * kWave + lane];
+                    in.xb = ntB ? w0c : my_st[rB * kWave + lane];
+                } else {
+                    in.xa = (ntA ? my_st0 : my_st)[rA * kWave + lane];
+                    in.xb = (ntB ? my_st0 : my_st)[rB * kWave + lane];
+                }
                 in.srca = (ntA ? srcA_nxt : srcA_cur)[cA];
                 in.srcb = (ntB ? srcB_nxt : srcB_cur)[8 + cA];
             } else {
-                in.xa = my_st[sl * kWave + lane];
-                in.xb = my_st[(8 + sl) * kWave + lane];
+                in.xa = my_st[rA * kWave + lane];
+                in.xb = my_st[rB * kWave + lane];
                 in.srca = in.srcb = 0.0;
             }
             in.ca = sm.cc[k][cA];
@@ -1399,28 +1454,23 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             nBy = onB1;
             // ---- outputs (a half that has not started keeps its step-0 state)
             const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
-            const int sl = s & 7;
-            if (tau >= 0) my_st[sl * kWave + lane] = outA;
-            if (tau >= 8) my_st[(8 + sl) * kWave + lane] = outB;
-            const unsigned eB = eA >= 8u ? eA - 8u : eA + Lu - 8u;
+            const int wA = PSW ? (s & 15) : (s & 7), wB = (PSW ? 16 : 8) + wA;
+            if (tau >= 0) my_st[wA * kWave + lane] = outA;
+            if (tau >= 8) my_st[wB * kWave + lane] = outB;
             keep_prev();
-            unsigned ra = vA ? eA * 1024u + lane16 : kOOB, rb = vB ? eB * 1024u + lane16 : kOOB;
+            unsigned ra = kOOB, rb = kOOB;
             v4u ka = outA, kb = outB;
-#if BURG_AB_PAIR_OOB
-            ra = rb = kOOB;
-#endif
-#if BURG_AB_PAIR_SMALL
-            ra &= 0x3FFFu;
-            rb &= 0x3FFFu;
-#endif
-#if !BURG_AB_PAIR_NORING
-            launder(ra);
-            launder(rb);
-            st_plain(ring, ra, ka);
-            st_plain(ring, rb, kb);
-#endif
-            eA += atE ? 9u : 1u;
-            if (eA >= Lu) eA -= Lu;
+            if constexpr (!PSW) {  // (PSW: the store wave stores them)
+                const unsigned eB = eA >= 8u ? eA - 8u : eA + Lu - 8u;
+                ra = vA ? eA * 1024u + lane16 : kOOB;
+                rb = vB ? eB * 1024u + lane16 : kOOB;
+                launder(ra);
+                launder(rb);
+                st_plain(ring, ra, ka);
+                st_plain(ring, rb, kb);
+                eA += atE ? 9u : 1u;
+                if (eA >= Lu) eA -= Lu;
+            }
             // east edge: B's column 15 (step qB)
             const bool out_e = atE & vB & rowok;
             v4u eo = as_v4u(oeB0, oeB1);
@@ -1433,6 +1483,11 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             }
             unsigned offA = kOOB, offB = kOOB;
             // north edge: the top lane's A (step qA, column cA) and B (qB, 8 + cA)
+            // (the kept north data assigned on every path: a value kept only
+            // on some paths is copied into a loop register of its own, and
+            // the store then reads the copy's source -- unkept)
+            kq_na = as_v4u(onA0, onA1);
+            kq_nb = as_v4u(onB0, onB1);
             if (has_north) {
                 const bool tl = lane == top;
                 offA = (tl & vA & (cA < ncol_real))
@@ -1441,8 +1496,6 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 offB = (tl & vB & (8 + cA < ncol_real))
                            ? nb + (unsigned)((a.qbase + qB) & (kR - 1)) * nstep + (unsigned)(8 + cA) * ncol
                            : kOOB;
-                kq_na = as_v4u(onA0, onA1);
-                kq_nb = as_v4u(onB0, onB1);
                 launder(offA);
                 launder(offB);
                 st_sys(nrs, offA, kq_na);
@@ -1499,11 +1552,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             const unsigned eoff = east_glob ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             // ring: A's entry at diagonal u is eA + u (+ 8 from uw8 on); B's is 8 below
             // (rA*: byte offsets -- not oA*, the cells' outputs below)
-#if BURG_AB_PAIR_COAL
-            const unsigned rA1 = __builtin_amdgcn_readfirstlane(eA) * 1024u + lane16, rA2 = rA1 + 8192u;
-#else
             const unsigned rA1 = eA * 1024u + lane16, rA2 = rA1 + 8192u;
-#endif
             // north (top lane): A at (step, column) = (q0, c0 + u) before uw8, (q0 + 1, c0 + u - 8)
             // after; B one step earlier at column 8 + that
             const bool tl = has_north & (lane == top);
@@ -1518,11 +1567,13 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             const LDS v4u *const insA = has_south ? &sm.ins[k][m16 & (kNI - 1)] : &sm.win[0][0][0];
             const LDS v4u *const insB = has_south ? &sm.ins[k][(m16 - 8) & (kNI - 1)] : &sm.win[0][0][0];
             const double lbuA = SWEEP ? lbA : lb;  // (sweep: the lane's current trajectory's inlet term)
+            // state slots: read u, write u (PSW: write (sb mod 16) + u, read the other half)
+            const int swA = PSW ? (sb & 8) : 0, srA = PSW ? (swA ^ 8) : 0, oB = PSW ? 16 : 8;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int ci = (c0 + u) & 7;
                 const bool at0 = u == uw, atE = u == ue;
-                const v4u xa = my_st[u * kWave + lane], xb = my_st[(8 + u) * kWave + lane];
+                const v4u xa = my_st[(srA + u) * kWave + lane], xb = my_st[(oB + srA + u) * kWave + lane];
                 const v4u ca = sm.cc[k][ci], cb = sm.cc[k][8 + ci];
                 // (volatile: the comm wave deposits these -- a plain load could be
                 // hoisted above the readiness wait)
@@ -1563,24 +1614,19 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 nBx = onB0;
                 nBy = onB1;
                 const v4u outA = as_v4u(oA0, oA1), outB = as_v4u(oB0, oB1);
-                my_st[u * kWave + lane] = outA;
-                my_st[(8 + u) * kWave + lane] = outB;
+                my_st[(swA + u) * kWave + lane] = outA;
+                my_st[(oB + swA + u) * kWave + lane] = outB;
                 keep_prev();
-                unsigned rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u, rB = rA - 8192u;
+                unsigned rA = kOOB, rB = kOOB;
                 v4u ka = outA, kb = outB;
-#if BURG_AB_PAIR_OOB
-                rA = rB = kOOB;
-#endif
-#if BURG_AB_PAIR_SMALL
-                rA &= 0x3FFFu;
-                rB &= 0x3FFFu;
-#endif
-#if !BURG_AB_PAIR_NORING
-                launder(rA);
-                launder(rB);
-                st_plain(ring, rA, ka);
-                st_plain(ring, rB, kb);
-#endif
+                if constexpr (!PSW) {  // (PSW: the store wave stores them)
+                    rA = (u < uw8 ? rA1 : rA2) + (unsigned)u * 1024u;
+                    rB = rA - 8192u;
+                    launder(rA);
+                    launder(rB);
+                    st_plain(ring, rA, ka);
+                    st_plain(ring, rB, kb);
+                }
                 v4u eo = as_v4u(oeB0, oeB1);
                 lds_st(atE ? eaddr : dumpv, eo);
                 unsigned eo_off = atE ? eoff : kOOB;
@@ -1607,8 +1653,10 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 kq_ob = ob;
             }
             if (has_west) lds_st(&src_w[qw & (kRL - 1)][lane], lempty);
-            eA += 16u;
-            if (eA >= Lu) eA -= Lu;
+            if constexpr (!PSW) {
+                eA += 16u;
+                if (eA >= Lu) eA -= Lu;
+            }
         };
         __builtin_amdgcn_s_waitcnt(0);  // (the prologue's global loads land here)
         for (int sb = 0; sb < total2; sb += U) {
@@ -1650,8 +1698,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 if (paborted) break;
             }
             if (sb == 0 && lane == 0) diag_first(a, south_host);
-            bool steady = (a.pair == 1) & (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W)) &
-                          !any_lane((eA < 8u) | (eA + 15u >= Lu));
+            bool steady = (a.pair == 1) & (nrow == kWave) & (sb >= 72) & (sb + U <= K8) & (!has_north | (ncol_real >= W));
+            if constexpr (!PSW) steady = steady & !any_lane((eA < 8u) | (eA + 15u >= Lu));
             if constexpr (SWEEP)
                 steady = steady & !any_lane((((sb + U - 1 - lane) >> 3) >= qnA) | ((((sb + U - 1 - lane) >> 3) - 1) >= qnB));
             if (steady) {
@@ -1680,9 +1728,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 lds_st(((lane < 16) & (d >= 0) & (d < KW)) ? &sm.ins[k][d & (kNI - 1)] : dumpv, lempty);
             }
         }
-#if BURG_AB_PAIR_SWEMU
-        lds_sti(lane == 0 ? &sm.prog[k] : sink, total2 + U);
-#endif
+        // (PSW: the store wave copies up to the last block)
+        if constexpr (PSW) lds_sti(lane == 0 ? &sm.prog[k] : sink, total2 + U);
         if (lane == 0) {
             if (pspins) atomicAdd(&a.stats->stall_spins, pspins);
             if (pslow) atomicAdd(&a.stats->slow_diagonals, pslow);
@@ -2032,9 +2079,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // (LDS writes go to a selected address -- a dump slot for lanes
         // that have nothing to write -- instead of an exec-masked branch)
         if constexpr (SE) {
-            if constexpr (!SE_G) lds_st(atE ? se_eaddr : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
+            if constexpr (!SE_G) lds_st(atE ? se_eaddr : &sm.dump[lane & (Img::kDump - 1)], eo);
         } else if constexpr (WIDE) {
-            if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], eo);
+            if (EDGE && east_lds) lds_st(out_e ? &sm.ewe[k][q & (kRL - 1)][lane] : &sm.dump[lane & (Img::kDump - 1)], eo);
         } else {
             if (east_lds && out_e) lds_st(&sm.ewe[k][q & (kRL - 1)][lane], eo);
         }
@@ -2092,7 +2139,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
         // consumed inbound slots back to empty (steady-edge blocks: once per
         // block, run_block)
         if constexpr (WIDE || STEADY) {
-            if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], lempty);
+            if (EDGE && has_west) lds_st(need_w ? &src_w[q & (kRL - 1)][lane] : &sm.dump[lane & (Img::kDump - 1)], lempty);
             // (the south slots are freed once per block, run_block)
         } else {
             if (need_w) lds_st(&src_w[q & (kRL - 1)][lane], lempty);
@@ -2165,7 +2212,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 se_in = has_west & (se_uw < U);
                 const bool oute = se_ue < U;
                 se_gw = lds_ld(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.zero);
-                se_eaddr = (east_lds & oute) ? &sm.ewe[k][qe & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
+                se_eaddr = (east_lds & oute) ? &sm.ewe[k][qe & (kRL - 1)][lane] : &sm.dump[lane & (Img::kDump - 1)];
                 se_eoff = (east_glob & oute) ? eb + (unsigned)((a.qbase + qe) & (kR - 1)) * (kWave * G) : kOOB;
             }
             const Bases b = bases_of(sb);
@@ -2202,19 +2249,19 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
             }
             // SteadyEdge: the west granule consumed in this block back to empty
             if (decltype(tag)::value >= 3 && has_west)
-                lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)], lempty);
+                lds_st(se_in ? &src_w[se_qw & (kRL - 1)][lane] : &sm.dump[lane & (Img::kDump - 1)], lempty);
         }
         if constexpr (WIDE || decltype(tag)::value >= 3) {
             // the block's south inbox slots back to empty, one write: lane i
             // frees diagonal sb + i's slot
             if (has_south)
-                lds_st(((lane < U) & (sb + lane < KW)) ? &sm.ins[k][(sb + lane) & (kNI - 1)] : &sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)],
+                lds_st(((lane < U) & (sb + lane < KW)) ? &sm.ins[k][(sb + lane) & (kNI - 1)] : &sm.dump[lane & (Img::kDump - 1)],
                        lempty);
         }
     };
 
     const int total = KW + kWave - 1;
-    LDS int *const sink_i = (LDS int *)&sm.dump[lane & (PipeLds<W, SWEEP>::kDump - 1)];
+    LDS int *const sink_i = (LDS int *)&sm.dump[lane & (Img::kDump - 1)];
     // Land the prologue's global loads (row coefficients) here: a first use
     // inside the loop would put an s_waitcnt vmcnt(0) -- a wait on every store
     // in flight -- into every diagonal.
@@ -2371,6 +2418,12 @@ const void *pipe_pair_fn(bool sweep)
     return sweep ? (const void *)pipe_kernel<16, true, true> : (const void *)pipe_kernel<16, false, true>;
 }
 
+size_t pipe_pair_image(bool sweep)
+{
+    constexpr bool psw = store_wave_of<16>();
+    return sweep ? sizeof(PipeLds<16, true, psw>) : sizeof(PipeLds<16, false, psw>);
+}
+
 const void *pipe_narrow_fn(int W, bool sweep)
 {
     if (sweep) return W == 8 ? (const void *)pipe_kernel<8, true> : W == 16 ? (const void *)pipe_kernel<16, true> : nullptr;
@@ -2446,9 +2499,11 @@ size_t image_of(int W)
 }
 
 // LDS bytes per workgroup: the image, padded for the wide-tile engine so that
-// exactly `per_cu` workgroups share a CU (narrow tiles keep their image size)
-size_t pipe_dyn_lds(int W, bool sweep, int per_cu)
+// exactly `per_cu` workgroups share a CU (narrow tiles keep their image size;
+// pair: the paired kernel's image)
+size_t pipe_dyn_lds(int W, bool sweep, int per_cu, bool pair = false)
 {
+    if (pair) return pipe_pair_image(sweep);
     const size_t img = sweep ? image_of<true>(W) : image_of<false>(W);
     if (W <= 16) return img;
     const size_t lds_cu = 160 * 1024;
@@ -2515,6 +2570,11 @@ int pipe_block_of(int W)
 }
 bool pipe_sweep_width_supported(int W) { return pipe_fn(W, true) != nullptr; }
 
+// the paired sweep kernel runs with a store wave and starts every trajectory
+// from a uniform initial state (PipeArgs::w0c): pipe_args pairs a sweep only
+// when the uploaded state is uniform
+bool pipe_pair_sweep_uniform_only() { return store_wave_of<16>(); }
+
 // resident workgroups of the pipe kernel (sweep = the burg_sweep variant,
 // whose larger LDS image must also fit one workgroup per CU)
 int pipe_max_resident_blocks(int W, bool sweep)
@@ -2532,8 +2592,9 @@ int pipe_max_resident_blocks(int W, bool sweep)
         return -3;
     if (W == 16) {  // the paired-halves build of the same plan must fit as well
         int np = 0;
-        if (!set_lds_limit(pipe_pair_fn(sweep), dyn) ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, pipe_pair_fn(sweep), 5 * kWave, dyn) != hipSuccess)
+        const size_t dp = pipe_dyn_lds(16, sweep, 1, true);
+        if (dp > 160 * 1024 || !set_lds_limit(pipe_pair_fn(sweep), dp) ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&np, pipe_pair_fn(sweep), pipe_threads(16), dp) != hipSuccess)
             return -3;
         n = std::min(n, np);
     }
@@ -2548,7 +2609,7 @@ int launch_pipe(const PipeArgs &a, int W, hipStream_t st)
     if (a.pair && (W != 16 || a.ret_k != 0)) return -1;
     const void *fn = a.pair ? pipe_pair_fn(sweep) : pipe_fn(W, sweep);
     if (!fn) return -1;
-    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W));
+    const size_t dyn = pipe_dyn_lds(W, sweep, pipe_per_cu_opt(W), a.pair != 0);
     if (dyn > 160 * 1024 || !set_lds_limit(fn, dyn)) return -1;
     // the census counter starts at zero in every launch
     if (hipMemsetAsync(a.census, 0, sizeof(unsigned), st) != hipSuccess) return -3;

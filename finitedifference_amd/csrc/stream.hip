@@ -440,6 +440,7 @@ __global__ void fill_sent_kernel(d2 *p, size_t n)
 // ring entry of state k (0: the launch's initial state), column cl, lane
 __device__ __forceinline__ long long ring_entry(const StreamArgs &a, int W, int k, int cl, int lane)
 {
+    if (a.play && k >= 1) return ring_pos_paired(k - 1, cl, lane, a.origin, a.L);
     return ring_pos((long long)(k - 1) * W + cl + lane, a.origin, a.L, W, a.ret_k, a.ret_n,
                     a.ret_base);
 }

@@ -176,6 +176,12 @@ int burg_ring_audit(int W, int num_steps, int snap_every, int ring_cap, int64_t 
  * entries, checked against the per-diagonal walk and ring_pos; plain rings,
  * W = 16). */
 #define BURG_AUDIT_PAIRED 1
+/* BURG_AUDIT_PAIRED | BURG_AUDIT_PAIRED_LAYOUT: the paired kernel's store
+ * wave in a burg_sweep launch (ring of num_steps W + 2 W + 128 entries, every
+ * state kept): the halves of paired diagonal s at entries origin + 2 s and
+ * + 1 (ring_pos_paired), checked cell by cell against the extraction's
+ * mapping; the retained states are 1 .. num_steps (state 0: the uploaded w0). */
+#define BURG_AUDIT_PAIRED_LAYOUT 2
 int burg_ring_audit_ex(int W, int num_steps, int snap_every, int ring_cap, int flags,
                        int64_t *report);
 

@@ -109,3 +109,55 @@ def test_paired_sweep_matches_one_cell_and_oracle(gpu, orc, monkeypatch, nx, ny,
             ref, _, _ = _problem(orc, nx, ny, mu=mu).fom(np.ones(2 * nx * ny), T)
             for q in range(T + 1):
                 assert np.array_equal(out["1"][j][:, q], ref[q]), f"mu {mu} step {q}"
+
+
+def _store_wave_build():
+    from finitedifference_amd import _lib
+    return "BURG_STORE_WAVE=0" not in _lib.build_flags()
+
+
+@pytest.mark.parametrize("nx,ny,nmu,T", [(256, 128, 3, 7), (200, 70, 4, 5)])
+def test_paired_sweep_uniform_initial_state_not_one(gpu, orc, monkeypatch, nx, ny, nmu, T):
+    """The paired sweep kernel with its store wave restarts every trajectory
+    from the uniform initial state as a constant (PipeArgs::w0c, DESIGN.md
+    section 4.1g): with u0 = 1.5, v0 = 0.5 (not the reference's ones) every
+    trajectory bit-equal to the oracle's and to the one-cell sweep."""
+    from finitedifference_amd.config import get_snapshot_params
+    mus = get_snapshot_params()[:nmu]
+    n = nx * ny
+    w0 = np.concatenate([np.full(n, 1.5), np.full(n, 0.5)])
+    out = {}
+    for pair in ("1", "0"):
+        monkeypatch.setenv("BURG_PAIR", pair)
+        ctx = _ctx(nx, ny, engine="pipe", stream_w=16)
+        ctx.upload(w0)
+        snaps, st = ctx.sweep(mus, T)
+        assert (st["paired_launches"] > 0) == (pair == "1")
+        out[pair] = snaps
+        ctx.close()
+    for j, mu in enumerate(mus):
+        assert np.array_equal(out["1"][j], out["0"][j]), f"mu {j}"
+        ref, _, _ = _problem(orc, nx, ny, mu=mu).fom(w0, T)
+        for q in range(T + 1):
+            assert np.array_equal(out["1"][j][:, q], ref[q]), f"mu {mu} step {q}"
+
+
+def test_paired_sweep_refused_for_nonuniform_initial_state(gpu, orc, monkeypatch):
+    """A non-uniform initial state has no constant to restart from: the sweep
+    runs one-cell even with BURG_PAIR=1 (store-wave builds; a
+    BURG_STORE_WAVE=0 build pairs it, its kernel keeps st0), and every
+    trajectory is the oracle's."""
+    from finitedifference_amd.config import get_snapshot_params
+    nx, ny, nmu, T = 200, 70, 3, 5
+    mus = get_snapshot_params()[:nmu]
+    w0 = planted_w0(nx, ny)
+    monkeypatch.setenv("BURG_PAIR", "1")
+    ctx = _ctx(nx, ny, engine="pipe", stream_w=16)
+    ctx.upload(w0)
+    snaps, st = ctx.sweep(mus, T)
+    ctx.close()
+    assert (st["paired_launches"] > 0) == (not _store_wave_build())
+    for j, mu in enumerate(mus):
+        ref, _, _ = _problem(orc, nx, ny, mu=mu).fom(w0, T)
+        for q in range(T + 1):
+            assert np.array_equal(snaps[j][:, q], ref[q]), f"mu {mu} step {q}"

@@ -97,3 +97,24 @@ def test_build_id_matches_checkout():
     """The library in the tree was built from the sources in the tree
     (burg_build_id vs the digest of csrc/ + Makefile + include/burgers.h)."""
     assert _lib.build_id() == _lib.source_id()
+
+
+# the paired kernel's store wave in burg_sweep launches writes the paired
+# sweep layout (ring_pos_paired: each half of a paired diagonal one
+# contiguous entry; DESIGN.md section 4.1g): every cell's entry in range,
+# equal to the extraction's mapping, and still holding its cell at the end
+@pytest.mark.parametrize("T", [3, 13, 500, 4500])
+def test_paired_sweep_layout_in_range_and_consistent(T):
+    r = _lib.ring_audit(16, T, 1, 0, paired=True, paired_layout=True)
+    assert r["accesses"] >= 2 * 8 * T * 64, r
+    assert r["out_of_range"] == 0 and r["walk_mismatch"] == 0, r
+    assert r["retained_overwritten"] == 0, r
+    assert r["retained_states"] == T, r
+    assert r["max_entry"] < r["entries_per_tile"], r
+
+
+def test_paired_sweep_layout_needs_the_paired_walk():
+    with pytest.raises(_lib.BurgersError):
+        _lib.ring_audit(16, 13, 1, 0, paired=False, paired_layout=True)
+    with pytest.raises(_lib.BurgersError):
+        _lib.ring_audit(16, 13, 2, 0, paired=True, paired_layout=True)
