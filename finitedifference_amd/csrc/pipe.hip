@@ -1160,40 +1160,56 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                 pw4[k] = (unsigned)a.origin;
                 rc4[k].init(a, W, 0);
             }
-            v4u kv[U];  // the previous block's store data and offsets, kept live (store VGPRs)
-            unsigned ko[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                kv[u] = v4u{0u, 0u, 0u, 0u};
-                ko[u] = 0u;
-            }
+            // Store VGPRs: waves k = 0, 2 copy through
+            // array x, k = 1, 3 through y, and the wave drains its stores
+            // (vmcnt(0)) before it reloads either -- at k = 2 and at the end
+            // of a pass -- with both arrays kept live until then.  A full
+            // block (every lane inside the launch, no wrap) stores at a lane
+            // offset plus a scalar entry offset: no per-lane address math.
             static_assert(U == 8, "store wave: blocks of 8");
+            const unsigned lane16 = lane * 16u;
+            auto keep = [](const v4u (&v)[U], const unsigned (&o)[U]) {
+                asm volatile("" ::"v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]),
+                             "v"(v[7]));
+                asm volatile("" ::"v"(o[0]), "v"(o[1]), "v"(o[2]), "v"(o[3]), "v"(o[4]), "v"(o[5]), "v"(o[6]),
+                             "v"(o[7]));
+            };
             long long t_prog = now_rt();
             for (;;) {
                 bool left = false, any = false;
+                v4u x[U], y[U];
+                unsigned ox[U], oy[U];  // (per-lane offsets: ramp and tail blocks)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
+                    if (k == 2) {
+                        // (k = 0's and 1's stores complete before x, y are reloaded)
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        keep(x, ox);
+                        keep(y, oy);
+                    }
+                    v4u(&v)[U] = (k & 1) ? y : x;
+                    unsigned(&o)[U] = (k & 1) ? oy : ox;
                     if (k >= nval) continue;
                     if (cp[k] < totalb && cp[k] + U <= lds_ldi(&sm.prog[k])) {
                         const __amdgpu_buffer_rsrc_t ring =
                             rsrc(a.ring + (size_t)(ti * ntj + tj0 + k) * a.Lt * kWave, (size_t)a.Lt * kWave * 16);
                         unsigned e = ret ? rc4[k].next(a, W, U) : pw4[k];
-                        v4u v[U];
 #pragma unroll
                         for (int u = 0; u < U; ++u) v[u] = lds_ld(&sm.st[k][(cp[k] + u) & (W - 1)][lane]);
-                        asm volatile("" ::"v"(kv[0]), "v"(kv[1]), "v"(kv[2]), "v"(kv[3]), "v"(kv[4]), "v"(kv[5]),
-                                     "v"(kv[6]), "v"(kv[7]));
-                        asm volatile("" ::"v"(ko[0]), "v"(ko[1]), "v"(ko[2]), "v"(ko[3]), "v"(ko[4]), "v"(ko[5]),
-                                     "v"(ko[6]), "v"(ko[7]));
+                        // (a retained-window block's U entries are consecutive)
+                        if (cp[k] >= kWave && cp[k] + U <= KW && (ret || e + U <= Lu)) {
 #pragma unroll
-                        for (int u = 0; u < U; ++u) {
-                            const int t = cp[k] + u - lane;
-                            unsigned o = (unsigned)t < (unsigned)KW ? e * 1024u + lane * 16u : kOOB;
-                            launder(o);
-                            st_plain(ring, o, v[u]);
-                            kv[u] = v[u];
-                            ko[u] = o;
-                            e = (!ret && e + 1 == Lu) ? 0u : e + 1;
+                            for (int u = 0; u < U; ++u) st_plain_so(ring, lane16, (e + u) * 1024u, v[u]);
+                            e += U;
+                            if (!ret && e == Lu) e = 0u;
+                        } else {
+#pragma unroll
+                            for (int u = 0; u < U; ++u) {
+                                const int t = cp[k] + u - lane;
+                                o[u] = (unsigned)t < (unsigned)KW ? e * 1024u + lane16 : kOOB;
+                                st_plain(ring, o[u], v[u]);
+                                e = (!ret && e + 1 == Lu) ? 0u : e + 1;
+                            }
                         }
                         if (!ret) pw4[k] = e;
                         cp[k] += U;
@@ -1204,6 +1220,9 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                     }
                     left |= cp[k] < totalb;
                 }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                keep(x, ox);
+                keep(y, oy);
                 if (!left || lds_ldi(&sm.perm[5])) break;
                 const long long tn = now_rt();
                 if (any) {
