@@ -1111,6 +1111,27 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                                     if ((unsigned)(tau - 8) < (unsigned)K8) st_plain_so(ring, lane16, eq1 * 1024u, v[U + u]);
                                     eq = eq1 + 1u == Lu ? 0u : eq1 + 1u;
                                 }
+                            } else if (sb >= 72 && sb + U <= K8 &&
+                                       !any_lane((eA4[k] < 8u) | (eA4[k] + 15u >= Lu))) {
+                                // standard layout, full block, no wrap (the
+                                // compute waves' former steady block): A at
+                                // the lane's entry + u (+ 8 once its column
+                                // wraps), B 8 entries below; u * 1 KB as the
+                                // scalar offset
+                                const unsigned e = eA4[k];
+                                const int c0 = (sb - lane) & 7;
+                                const int uw8 = c0 == 0 ? 8 : ((8 - c0) & 7);
+                                const unsigned rA1 = e * 1024u + lane16, rA2 = rA1 + 8192u, rB1 = rA1 - 8192u;
+#pragma unroll
+                                for (int u = 0; u < U; ++u) {
+                                    o[u] = u < uw8 ? rA1 : rA2;
+                                    o[U + u] = u < uw8 ? rB1 : rA1;
+                                    st_plain_so(ring, o[u], (unsigned)u * 1024u, v[u]);
+                                    st_plain_so(ring, o[U + u], (unsigned)u * 1024u, v[U + u]);
+                                }
+                                // (per-lane offsets: drained before they are reused)
+                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                                eA4[k] = e + 16u >= Lu ? e + 16u - Lu : e + 16u;
                             } else {
                                 unsigned e = eA4[k];
 #pragma unroll
@@ -1124,6 +1145,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                                     e += (tau & 7) == 7 ? 9u : 1u;
                                     if (e >= Lu) e -= Lu;
                                 }
+                                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                                 eA4[k] = e;
                             }
                             ep4[k] = ep + 2u * U >= Lu ? ep + 2u * U - Lu : ep + 2u * U;
@@ -1210,6 +1232,8 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                                 st_plain(ring, o[u], v[u]);
                                 e = (!ret && e + 1 == Lu) ? 0u : e + 1;
                             }
+                            // (per-lane offsets: drained before they are reused)
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         }
                         if (!ret) pw4[k] = e;
                         cp[k] += U;

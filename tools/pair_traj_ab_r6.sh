@@ -2,16 +2,18 @@
 # Paired single trajectories after the paired store wave (standard layout,
 # per-lane walk, drained per block): the whole GPU
 # suite, then one 1024^2 x 1500 trajectory (paired by default: K >= (nx +
-# rows) / 2) on the default build, on the build before the paired store wave
+# rows) / 2; BURG_PAIR=1 set explicitly) on the default build, on the build before the paired store wave
 # (libburgers_hip_prev.so) and one-cell (BURG_PAIR=0), 3 interleaved rounds.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/${TAG:-ab_ptraj}; mkdir -p $O
+if [ -z "$SKIP_SUITE" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
+fi
 for r in 1 2 3; do for v in prev new onecell; do
   L=$PWD/finitedifference_amd/libburgers_hip.so; [ $v = prev ] && L=$PWD/finitedifference_amd/libburgers_hip_prev.so
-  P=""; [ $v = onecell ] && P=0
+  P=1; [ $v = onecell ] && P=0
   BURG_PAIR=$P BURG_LIB=$L timeout -k 10 300 python3 -c "
 import json, bench, numpy as np
 from finitedifference_amd.solver import FOMContext
