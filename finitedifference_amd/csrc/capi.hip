@@ -643,7 +643,7 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
     // its steady blocks, diagnostics).
     {
         const char *e = std::getenv("BURG_PAIR");
-        int pair_opt = e ? std::atoi(e) : -1;
+        int pair_opt = (e && *e) ? std::atoi(e) : -1;  // (set but empty: the default)
         if (pair_opt < 0) pair_opt = (a.T < K || 2LL * K >= (long long)c->nx + c->nrows) ? 1 : 0;
         a.pair = (pair_opt == 1 || pair_opt == 2) && c->sp.W == 16 && a.ret_k == 0 ? pair_opt : 0;
         // the paired sweep kernel (with its store wave) restarts trajectories
@@ -655,7 +655,7 @@ PipeArgs pipe_args(burg_ctx *c, long long L, long long origin, int K, const Traj
         // (ring_pos_paired: contiguous 1 KB entries; the sweep's extraction
         // reads it); BURG_PAIR_LAYOUT=0 keeps the standard one (A/B)
         const char *pl = std::getenv("BURG_PAIR_LAYOUT");
-        a.play = (a.pair && a.colc_b && pipe_pair_sweep_uniform_only() && !(pl && std::atoi(pl) == 0)) ? 1 : 0;
+        a.play = (a.pair && a.colc_b && pipe_pair_sweep_uniform_only() && !(pl && *pl && std::atoi(pl) == 0)) ? 1 : 0;
     }
     a.spin_ticks = c->spin_ticks;
     a.census_ticks = std::min<long long>(c->spin_ticks, 100000000LL);  // <= 1 s
