@@ -71,7 +71,8 @@ struct StreamStats {
     unsigned long long slow_ticks;      // s_memtime ticks spent in the slow path
     unsigned long long why[6];          // slow-path causes: 0 east slot busy, 1 north slot
                                         // busy, 2 west not written, 3 south not written,
-                                        // 4 range (IEEE redo), 5 entries that needed a re-poll
+                                        // 4 range (IEEE redo; pipe: the loader window or the
+                                        // store wave), 5 entries that needed a re-poll
     unsigned long long nonfinite_diagonals;  // diagonals whose new state has a NaN / Inf
     unsigned long long prof[8];  // pipe, built with -DBURG_PIPE_PROF: compute-wave clocks in
                                  // [0] the loop, [1] block-start store waits, [2] readiness

@@ -805,7 +805,7 @@ int stream_stats_end(burg_ctx *c, burg_stats *st, int64_t steps, int64_t launche
                 std::fprintf(stderr,
                              c->eng_eff == BURG_ENGINE_PIPE
                                  ? "[pipe] blocks that waited, by missing kind: east %llu north %llu "
-                                   "west %llu south %llu window %llu; comm polls %llu\n"
+                                   "west %llu south %llu window / store wave %llu; comm polls %llu\n"
                                  : "[stream] slow-path causes: east-busy %llu north-busy %llu "
                                    "west-unwritten %llu south-unwritten %llu range %llu repoll %llu\n",
                              ss.why[0], ss.why[1], ss.why[2], ss.why[3], ss.why[4], ss.why[5]);

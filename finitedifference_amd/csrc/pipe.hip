@@ -1720,6 +1720,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                         pwhy[1] += (why & 16u) != 0;
                         pwhy[2] += (why & 1u) != 0;
                         pwhy[3] += (why & 2u) != 0;
+                        pwhy[4] += (why & 64u) != 0;  // the store wave (PSW)
                         wsouth = (why & 2u) != 0;
                     } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                         if (lane == 0 && !lds_ldi(&sm.perm[5])) {
@@ -2348,7 +2349,7 @@ __global__ __launch_bounds__(threads_of<W>()) __attribute__((amdgpu_waves_per_eu
                     wait_why[1] += (why & 16u) != 0;  // north grant
                     wait_why[2] += (why & 1u) != 0;   // west inflow
                     wait_why[3] += (why & 2u) != 0;   // south inflow
-                    wait_why[4] += (why & 32u) != 0;  // previous states (loader window)
+                    wait_why[4] += (why & 96u) != 0;  // previous states (loader window) / the store wave
                     wsouth = (why & 2u) != 0;
                 } else if (lds_ldi(&sm.perm[5]) || now_rt() - t0 > a.spin_ticks) {
                     if (lane == 0 && !lds_ldi(&sm.perm[5])) {
